@@ -1,0 +1,292 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/*.npz by running the REFERENCE (SmithB/LSsurf at
+/root/reference) in the survey container.
+
+Only this script touches the reference; it is a no-op where /root/reference is absent (the
+GPU box).  The reference is imported with the stand-ins of tests/golden/_refstubs.py:
+pointCollection containers, and sparseqr.solve/rz = the exact dense LS oracle (oracle/dense.py)
+because SuiteSparseQR/PySPQR are unavailable (parity at that boundary rests on uniqueness of the
+full-rank LS solution).  Fixtures hold inputs and outputs only — no reference code.
+
+Fixtures
+--------
+stencils.npz   lin_op triplets (r, c, v, ind0) for every stencil/interp operator on tiny grids
+               (lin_op.py:80-309, 163-247), vstack/toCSR of a composite (lin_op.py:555-631,745-753)
+sys_*.npz      for each smooth_fit / lin_op configuration: the input points, the exact matrix A
+               and rhs b that the reference handed to sparseqr.solve (smooth_fit.py:142), the
+               exact LS solution x*, and the smooth_fit outputs (z0, dz, z_est, three_sigma_edit,
+               sigma_extra, dzdt_lag1, E sigma grids)
+tri.npz        I/O of the reference Cython kernels inv_tr_upper / propagate_qz_errors /
+               spsolve_tr_upper on random upper-triangular CSR matrices (incl. overflow)
+kat.npz        the analytic amplitude KAT of notebooks/smooth_fit_demo.ipynb cell 8
+"""
+import os
+import sys
+
+import numpy as np
+import scipy.sparse as sp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+E_RMS_NB = {'d2z0_dx2': 0.03, 'dz0_dx': 75., 'd3z_dx2dt': 0.006, 'd2z_dxdt': 15., 'd2z_dt2': 5000.}
+
+
+def _csr_arrays(prefix, A):
+    A = sp.csr_matrix(A)
+    A.sum_duplicates()
+    A.sort_indices()
+    return {prefix + '_indptr': A.indptr.astype(np.int64), prefix + '_indices': A.indices.astype(np.int32),
+            prefix + '_data': A.data, prefix + '_shape': np.array(A.shape)}
+
+
+def gen_stencils(LS):
+    out = {}
+    g2 = LS.fd_grid([[0., 400.], [0., 500.]], [100., 100.], name='z0')
+    g3 = LS.fd_grid([[0., 300.], [0., 400.], [0., 1.25]], [100., 100., 0.25], name='dz', col_0=30)
+    ops = {
+        'grad2': LS.lin_op(g2, name='grad2_z0').grad2(DOF='z0'),
+        'grad': LS.lin_op(g2, name='grad_z0').grad(DOF='z0'),
+        'one': LS.lin_op(g2, name='mag_z0').one(DOF='z0'),
+        'grad2_dzdt': LS.lin_op(g3, name='grad2_dzdt').grad2_dzdt(DOF='z', t_lag=1),
+        'grad_dzdt': LS.lin_op(g3, name='grad_dzdt').grad_dzdt(DOF='z', t_lag=1),
+        'd2z_dt2': LS.lin_op(g3, name='d2z_dt2').d2z_dt2(DOF='z'),
+        'dzdt': LS.lin_op(g3, name='dzdt_lag1').dzdt(lag=1),
+        'dzdt2': LS.lin_op(g3, name='dzdt_lag2').dzdt(lag=2),
+    }
+    rng = np.random.default_rng(7)
+    y2 = np.r_[rng.uniform(0, 400, 40), 0., 400., 100., 400., 250.]
+    x2 = np.r_[rng.uniform(0, 500, 40), 0., 500., 200., 350., 500.]
+    out['pts2_y'], out['pts2_x'] = y2, x2
+    ops['interp2'] = LS.lin_op(g2, name='interp_z').interp_mtx([y2, x2])
+    y3 = np.r_[rng.uniform(0, 300, 40), 0., 300., 100.]
+    x3 = np.r_[rng.uniform(0, 400, 40), 0., 400., 200.]
+    t3 = np.r_[rng.uniform(0, 1.25, 40), 0., 1.25, 0.5]
+    out['pts3_y'], out['pts3_x'], out['pts3_t'] = y3, x3, t3
+    ops['interp3'] = LS.lin_op(g3, name='interp_dz').interp_mtx([y3, x3, t3])
+    for k, op in ops.items():
+        out[k + '_r'] = np.asarray(op.r).ravel()
+        out[k + '_c'] = np.asarray(op.c).ravel()
+        out[k + '_v'] = np.asarray(op.v).ravel()
+        out[k + '_ind0'] = np.asarray(op.ind0).ravel()
+        out[k + '_neq'] = np.array(op.N_eq)
+    Gc = LS.lin_op(None, name='constraints').vstack([ops['grad2'], ops['grad']])
+    out.update(_csr_arrays('vstack', Gc.toCSR()))
+    np.savez_compressed(os.path.join(HERE, 'stencils.npz'), **out)
+
+
+def synth_points(rng, W, ctr, n, with_t=True, outside=0):
+    """uniform points in the domain + a few exactly on bounds/nodes + `outside` out-of-bounds."""
+    x = ctr['x'] + (rng.random(n) - 0.5) * W['x']
+    y = ctr['y'] + (rng.random(n) - 0.5) * W['y']
+    t = ctr['t'] + (rng.random(n) - 0.5) * W['t']
+    # exact upper/lower bounds and an exact node
+    x[:3] = [ctr['x'] + W['x'] / 2, ctr['x'] - W['x'] / 2, ctr['x']]
+    y[:3] = [ctr['y'] + W['y'] / 2, ctr['y'], ctr['y'] - W['y'] / 2]
+    t[:3] = [ctr['t'] + W['t'] / 2, ctr['t'] - W['t'] / 2, ctr['t']]
+    if outside:
+        x[3:3 + outside] = ctr['x'] + W['x']          # out of bounds: dropped by smooth_fit
+    Lx, Ly = W['x'] / 2, W['y'] / 3
+    z = 10 * np.sin(2 * np.pi * x / Lx) * np.cos(2 * np.pi * y / Ly) \
+        + 0.5 * t * np.exp(-((x - ctr['x'])**2 + (y - ctr['y'])**2) / (W['x'] / 4)**2) \
+        + rng.normal(0, 0.1, n)
+    return x, y, t, z
+
+
+def run_sf(LS, stubs, name, data_dict, sf_kwargs, n_outliers=0, rng=None):
+    import pointCollection as pc
+    data = pc.data().from_dict(data_dict)
+    stubs.CALLS.clear()
+    S = LS.smooth_fit(data=data, **sf_kwargs)
+    out = {'in_' + k: np.asarray(v) for k, v in data_dict.items()}
+    A, b = stubs.CALLS[0]
+    out.update(_csr_arrays('A', A))
+    out['b'] = b
+    from oracle import dense
+    x = dense.ls_solve_dense(A, b)
+    out['x'] = x
+    out['x_opt'] = np.array(dense.optimality(A, b, x))
+    # last solve (after editing) as well
+    A2, b2 = stubs.CALLS[-1]
+    out.update(_csr_arrays('Alast', A2))
+    out['blast'] = b2
+    out['n_solves'] = np.array(len(stubs.CALLS))
+    m = S['m']
+    out['z0'] = m['z0'].z0
+    out['dz'] = m['dz'].dz
+    out['m_all'] = m['all']
+    d = S['data']
+    for f in ['z_est', 'three_sigma_edit', 'sigma_extra']:
+        out['data_' + f] = np.asarray(getattr(d, f))
+    out['valid_data'] = np.asarray(S['valid_data'])
+    for k in m:
+        if k.startswith('dzdt_lag'):
+            out['m_' + k] = getattr(m[k], k)
+    for f in ['count', 'misfit_rms', 'misfit_scaled_rms']:
+        out['z0_' + f] = getattr(m['z0'], f)
+        out['dz_' + f] = getattr(m['dz'], f)
+    for k, v in S['R'].items():
+        out['R_' + k] = np.array(v)
+    for k, v in S['RMS'].items():
+        out['RMS_' + k] = np.array(v)
+    for k, v in S['E'].items():
+        out['E_' + k] = np.asarray(getattr(v, k))
+    out['kwargs'] = np.array(repr({k: v for k, v in sf_kwargs.items()}))
+    np.savez_compressed(os.path.join(HERE, f'sys_{name}.npz'), **out)
+    print(f'{name}: A {A.shape} nnz {A.nnz}, solves {len(stubs.CALLS)}, opt {out["x_opt"]:.2e}')
+
+
+def gen_systems(LS, stubs):
+    rng = np.random.default_rng(20251121)
+    # 1. 3-D z0+dz, equal spacing (the C3/C4 structure at toy size)
+    W = {'x': 1500., 'y': 1500., 't': 1.25}
+    ctr = {'x': 0., 'y': 0., 't': 0.}
+    x, y, t, z = synth_points(rng, W, ctr, 700, outside=2)
+    run_sf(LS, stubs, 'sf3d', {'x': x, 'y': y, 'time': t, 'z': z, 'sigma': np.full(x.size, 0.1)},
+           dict(W=W, ctr=ctr, spacing={'z0': 100., 'dz': 100., 'dt': 0.25}, E_RMS=E_RMS_NB,
+                reference_epoch=3, max_iterations=1, VERBOSE=False, dzdt_lags=[1]))
+    # 2. finer z0 than dz, 'z0' magnitude constraint, outliers, 3 outer iterations
+    W = {'x': 1000., 'y': 800., 't': 1.0}
+    x, y, t, z = synth_points(rng, W, ctr, 900)
+    bad = rng.random(x.size) > 0.9
+    z[bad] += (rng.random(bad.sum()) - 0.5) * 40
+    E = dict(E_RMS_NB, z0=50.)
+    run_sf(LS, stubs, 'sf3d_edit', {'x': x, 'y': y, 'time': t, 'z': z, 'sigma': np.full(x.size, 0.1)},
+           dict(W=W, ctr=ctr, spacing={'z0': 50., 'dz': 100., 'dt': 0.25}, E_RMS=E,
+                reference_epoch=2, max_iterations=4, VERBOSE=False, dzdt_lags=[1, 2]))
+    # 3. notebooks/smooth_fit_demo.ipynb cell 17 (x-t problem), exactly
+    W = {'x': 1.e4, 'y': 200, 't': 2}
+    xx = np.arange(-W['x'] / 2, W['x'] / 2, 100)
+    amp, lam = 100, 2000
+    d0 = {'x': xx, 'y': np.zeros_like(xx), 'z': np.zeros_like(xx), 'time': np.zeros_like(xx) - 0.99,
+          'sigma': np.zeros_like(xx) + 1}
+    d1 = {'x': xx, 'y': np.zeros_like(xx), 'z': amp - amp * np.cos(2 * np.pi * xx / lam),
+          'time': np.zeros_like(xx) + 0.99, 'sigma': np.zeros_like(xx) + 1}
+    dd = {k: np.r_[d0[k], d1[k]] for k in d0}
+    E = dict(E_RMS_NB)
+    run_sf(LS, stubs, 'nb_xt', dd, dict(W=W, ctr=ctr, spacing={'z0': 50, 'dz': 100, 'dt': 0.25},
+                                         E_RMS=E, reference_epoch=4, max_iterations=1, VERBOSE=False,
+                                         dzdt_lags=[1]))
+    # 4. notebook cell 45: reduced-resolution error propagation (compute_E), data gap
+    gap = np.abs(dd['x']) > 1000
+    dg = {k: v[gap] for k, v in dd.items()}
+    run_sf(LS, stubs, 'nb_err', dg, dict(W={'x': 1.e4, 'y': 400, 't': 2}, ctr=ctr,
+                                          spacing={'z0': 100, 'dz': 200, 'dt': 0.25}, E_RMS=E,
+                                          reference_epoch=4, max_iterations=1, compute_E=True,
+                                          VERBOSE=False, dzdt_lags=[1]))
+
+
+def gen_lin2d(LS):
+    """2-D z0-only direct system (BASELINE config C2 structure), formed with the reference
+    lin_op exactly as notebooks/smooth_fit_demo_aniso.ipynb cell 6 does."""
+    rng = np.random.default_rng(20251122)
+    g = LS.fd_grid([[0., 2300.], [0., 2300.]], [100., 100.], name='z0')
+    n = 300
+    y, x = rng.uniform(0, 2300, n), rng.uniform(0, 2300, n)
+    z = 10 * np.sin(2 * np.pi * x / 1150) + rng.normal(0, 0.1, n)
+    sigma = np.full(n, 0.1)
+    G = LS.lin_op(g, name='interp_z').interp_mtx([y, x])
+    root = np.sqrt(np.prod(g.delta))
+    g2 = LS.lin_op(g, name='grad2_z0').grad2(DOF='z0')
+    g2.expected = 0.03 / root * np.ones(g2.N_eq)
+    g1 = LS.lin_op(g, name='grad_z0').grad(DOF='z0')
+    g1.expected = 75. / root * np.ones(g1.N_eq)
+    Gc = LS.lin_op(None, name='constraints').vstack([g2, g1])
+    Gcoo = sp.vstack([G.toCSR(), Gc.toCSR()]).tocoo()
+    Eall = np.concatenate([sigma, g2.expected, g1.expected])
+    rhs = np.concatenate([z, np.zeros(Gc.shape[0])])
+    TCinv = sp.dia_matrix((1 / Eall, 0), shape=(rhs.size, rhs.size))
+    A = TCinv.dot(Gcoo)
+    b = TCinv.dot(rhs)
+    from oracle import dense
+    xs = dense.ls_solve_dense(A, b)
+    out = {'in_x': x, 'in_y': y, 'in_z': z, 'in_sigma': sigma, 'b': b, 'x': xs,
+           'x_opt': np.array(dense.optimality(A, b, xs))}
+    out.update(_csr_arrays('A', A))
+    np.savez_compressed(os.path.join(HERE, 'sys_lin2d.npz'), **out)
+    print(f'lin2d: A {A.shape} nnz {A.nnz}, opt {out["x_opt"]:.2e}')
+
+
+def rand_upper(rng, N, density, diag_first=True):
+    R = sp.random(N, N, density=density, random_state=rng, format='csr')
+    R = sp.triu(R, k=1).tocsr()
+    R = R + sp.diags(rng.uniform(1.0, 3.0, N) * np.sign(rng.normal(size=N)))
+    R = sp.csr_matrix(R)
+    R.sort_indices()
+    return R
+
+
+def gen_tri(LS):
+    import importlib
+    itu = importlib.import_module('LSsurf.inv_tr_upper').inv_tr_upper
+    pqe = importlib.import_module('LSsurf.propagate_qz_errors').propagate_qz_errors
+    sst = importlib.import_module('LSsurf.spsolve_tr_upper').spsolve_tr_upper
+    rng = np.random.default_rng(99)
+    out = {}
+    cases = [(1, 1.0), (7, 0.5), (60, 0.08), (250, 0.02)]
+    for i, (N, dens) in enumerate(cases):
+        R = rand_upper(rng, N, dens)
+        out.update(_csr_arrays(f'R{i}', R))
+        nnz = max(4, N * N // 4)
+        rr, cc, vv, st = itu(R, nnz, 1e-5)
+        out[f'inv{i}_rr'], out[f'inv{i}_cc'], out[f'inv{i}_vv'], out[f'inv{i}_st'] = rr, cc, vv, np.array(st)
+        out[f'inv{i}_nnz'] = np.array(nnz)
+        # a too-small buffer: the overflow/status=1 semantics (smooth_fit.py:240-246 retries)
+        small = max(2, N // 2)
+        rr, cc, vv, st = itu(R, small, 1e-5)
+        out[f'ovf{i}_rr'], out[f'ovf{i}_cc'], out[f'ovf{i}_vv'], out[f'ovf{i}_st'] = rr, cc, vv, np.array(st)
+        out[f'ovf{i}_nnz'] = np.array(small)
+        out[f'rss{i}'] = pqe(R)
+        bb = rng.normal(size=N)
+        out[f'b{i}'] = bb
+        out[f'sol{i}'] = sst(R, bb)
+    out['ncases'] = np.array(len(cases))
+    np.savez_compressed(os.path.join(HERE, 'tri.npz'), **out)
+    print('tri: ok')
+
+
+def gen_kat(LS):
+    """notebooks/smooth_fit_demo.ipynb cells 4-8: recovered vs analytic sine amplitude."""
+    import pointCollection as pc
+    W = {'x': 1.e4, 'y': 200, 't': 2}
+    ctr = {'x': 0., 'y': 0., 't': 0.}
+    spacing = {'z0': 50, 'dz': 100, 'dt': 0.25}
+    x = np.arange(-W['x'] / 2, W['x'] / 2, 100)
+    lam, amp, sig = 2000, 100, 1
+    D = {'x': x, 'y': np.zeros_like(x), 'z': -amp * np.cos(2 * np.pi * x / lam),
+         'time': np.zeros_like(x) - 0.5, 'sigma': np.zeros_like(x) + sig}
+    dd = {k: np.r_[D[k], D[k]] for k in D}
+    dd['time'] = np.r_[D['time'], np.zeros_like(x) + 0.5]
+    E_RMS = {'d2z0_dx2': 0.06, 'dz0_dx': 0.06 * 2500, 'd3z_dx2dt': 0.0001, 'd2z_dxdt': 0.0001 * 2500,
+             'd2z_dt2': 5000}
+    rd = dd['x'].size / W['x'] / W['y']
+    Es, Am, Ae = [0.006, 0.001, 0.0003], [], []
+    for E in Es:
+        E_RMS['d2z0_dx2'] = E
+        S = LS.smooth_fit(data=pc.data().from_dict(dd), ctr=ctr, W=W, spacing=spacing, E_RMS=dict(E_RMS),
+                          reference_epoch=2, max_iterations=1, VERBOSE=False, dzdt_lags=[1])
+        z0 = S['m']['z0']
+        row = int(z0.z0.shape[0] / 2)
+        Am.append(np.max(np.abs(z0.z0[row, np.abs(z0.x) < 3000])))
+        Ae.append(amp / (1 + 16 * E**-2 * np.pi**4 / (lam**4 * rd) * sig**2))
+    np.savez_compressed(os.path.join(HERE, 'kat.npz'), E=np.array(Es), A_ref=np.array(Am),
+                        A_expected=np.array(Ae), **{'in_' + k: v for k, v in dd.items()})
+    print('kat:', Am, Ae)
+
+
+def main():
+    if not os.path.isdir('/root/reference'):
+        print('gen_golden: /root/reference absent; keeping committed fixtures')
+        return
+    import _refstubs
+    LS = _refstubs.install()
+    sys.modules['LSsurf.smooth_fit'].smooth_fit   # module (LSsurf/__init__.py:6 rebinds the name)
+    gen_stencils(LS)
+    gen_tri(LS)
+    gen_lin2d(LS)
+    gen_systems(LS, _refstubs)
+    gen_kat(LS)
+
+
+if __name__ == '__main__':
+    main()
