@@ -1,0 +1,138 @@
+/*
+ * lsqsurf.h — C ABI of lssurf_amd's MI355X (gfx950) least-squares solve path.
+ *
+ * This is the only public native surface (liblsqsurf.so).  It replaces, for LSsurf's
+ * sparse regularized least-squares solve path:
+ *
+ *   sparseqr.solve(A, b)               LSsurf/smooth_fit.py:142 (iterate_fit),
+ *                                      notebooks/smooth_fit_demo_aniso.ipynb cells 6,13,16,18,20
+ *       -> lsq_create / lsq_set_col_map / lsq_set_matrix_coo / lsq_set_row_weight /
+ *          lsq_set_row_mask / lsq_solve
+ *   G_data.toCSR().dot(m0)             LSsurf/smooth_fit.py:146,662 (residual / z_est)
+ *       -> lsq_spmv
+ *   Gcoo = sp.vstack([...]).tocoo()·Ip_c, TCinv·Gcoo, Ip_r·(...)   smooth_fit.py:613-627,123-142
+ *       -> formed on the device by lsq_set_matrix_coo (+col map, row weight, row mask)
+ *   inv_tr_upper(R, nnz, tol)          LSsurf/inv_tr_upper.pyx:19-94 (smooth_fit.py:240-246)
+ *       -> tri_upper_inv_csr
+ *   propagate_qz_errors(R)             LSsurf/propagate_qz_errors.pyx:15-69
+ *       -> tri_upper_rowrss_csr
+ *   spsolve_tr_upper(A, b)             LSsurf/spsolve_tr_upper.pyx:11-54
+ *       -> tri_upper_solve_csr
+ *
+ * Conventions
+ *   - Ownership: the caller owns every host buffer; the library copies in and out and owns all
+ *     device memory.  Pointers are plain host pointers, sizes are int64.
+ *   - Errors: int return, 0 = ok, 1 = "not converged" (lsq_solve hit maxit) or "output buffer
+ *     full" (tri_upper_inv_csr, same meaning as inv_tr_upper's status=1); < 0 = invalid
+ *     argument / call order / HIP error, with lsq_last_error() describing it.  There is no CPU
+ *     fallback: without a usable gfx950 device every call fails.
+ *   - Threading: one handle per host thread; calls on one handle are serialised.
+ */
+#ifndef LSQSURF_H
+#define LSQSURF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct lsq_handle lsq_handle;
+
+/* Solver options.  Defaults (lsq_default_opts) reproduce scipy.sparse.linalg.lsqr's stopping
+ * rules with atol = btol = 1e-10, conlim = 1e8, maxit = 4*n. */
+typedef struct lsq_opts {
+    int32_t method;        /* 0 = LSQR (Paige & Saunders 1982)                                 */
+    int32_t precond;       /* 0 = none, 1 = column (Jacobi) scaling                            */
+    double  atol, btol, conlim;
+    int64_t maxit;
+    int32_t use_x0;        /* 1: x_inout holds a warm start (outer-iteration "resume")          */
+    int32_t batch;         /* iterations per device batch between host convergence checks      */
+    int32_t use_graph;     /* 1: replay each batch as a captured hipGraph                       */
+    int32_t reserved;
+} lsq_opts;
+
+/* Statistics (mirrors scipy's lsqr return tuple, plus timing and the byte model). */
+typedef struct lsq_stats {
+    int64_t iters;
+    int32_t istop;         /* scipy istop: 1,2 converged; 3 cond limit; 4-6 machine precision; 7 maxit */
+    int32_t reserved;
+    double  r1norm, r2norm, anorm, acond, arnorm, xnorm;
+    double  time_s;        /* device-resident iteration time (A, b already in HBM)              */
+    double  bytes_per_iter;/* algorithmic HBM bytes of one LSQR iteration (DESIGN.md byte model)*/
+} lsq_stats;
+
+void        lsq_default_opts(lsq_opts* o);
+
+/* ---- handle lifetime -------------------------------------------------------------------- */
+lsq_handle* lsq_create(int32_t device);
+void        lsq_destroy(lsq_handle* h);
+const char* lsq_last_error(lsq_handle* h);     /* never NULL; "" when no error                 */
+
+/* ---- matrix formation (replaces the scipy assembly of smooth_fit.py:613-627) ------------ */
+/* Optional, before lsq_set_matrix_coo: keep only these columns of the full operator, in this
+ * order (= Ip_c of build_reference_epoch_matrix, constraint_functions.py:112-151). keep_cols
+ * must be strictly increasing in [0, n). */
+int lsq_set_col_map(lsq_handle* h, int64_t n_full, const int64_t* keep_cols, int64_t n_keep);
+
+/* Form A = diag(row_weight) * G * Ip_c on the device from COO triplets of G (m x n_full):
+ * entries with v == 0 are dropped, duplicates are summed in input order, sums equal to 0 are
+ * dropped, columns outside the col map are removed (lin_op.toCSR, lin_op.py:745-753, plus the
+ * scipy products of smooth_fit.py:613-627).  row_weight may be NULL (= 1).  Builds A and Aᵀ. */
+int lsq_set_matrix_coo(lsq_handle* h, int64_t m, int64_t n_full, int64_t nnz,
+                       const int64_t* r, const int64_t* c, const double* v,
+                       const double* row_weight);
+
+/* Replace the row weights (TCinv of iterate_fit, smooth_fit.py:123-129) without re-forming. */
+int lsq_set_row_weight(lsq_handle* h, const double* row_weight);
+/* Row selection Ip_r (smooth_fit.py:132-135): rows with keep[i] == 0 are excluded from the
+ * fit (treated as absent rows).  NULL keeps every row. */
+int lsq_set_row_mask(lsq_handle* h, const uint8_t* keep);
+
+int lsq_shape(lsq_handle* h, int64_t* m, int64_t* n, int64_t* nnz);
+/* Download the formed A (selected rows only, in row order; canonical CSR, sorted columns). */
+int lsq_get_csr(lsq_handle* h, int64_t* indptr, int32_t* indices, double* data);
+
+/* ---- solve and products ----------------------------------------------------------------- */
+/* x = argmin || A x - diag(row_weight)·mask·b ||.  b has length m (unweighted rhs, all rows);
+ * x_inout has length n (compacted columns).  Returns 0 converged, 1 maxit reached. */
+int lsq_solve(lsq_handle* h, const double* b, double* x_inout, const lsq_opts* o, lsq_stats* s);
+
+/* y = G x (trans = 0; x length n, y length m, UNWEIGHTED rows, all rows) or
+ * y = Gᵀ x (trans = 1).  G is the formed operator before row weights and row mask. */
+int lsq_spmv(lsq_handle* h, int32_t trans, const double* x, double* y);
+
+/* Bench / profiling hook: run exactly `iters` LSQR iterations on the current system (no early
+ * stop), starting from the state left by the previous call (first call initialises from b).
+ * Times only the device iterations. */
+int lsq_iterate(lsq_handle* h, const double* b, int64_t iters, const lsq_opts* o, lsq_stats* s);
+
+/* Bench / profiling hooks.  lsq_profile_kernels times each iteration kernel in isolation
+ * (reps launches each, HIP events on the handle's stream): ms4 = {x/w+SpMV, SpMTV, beta reduce,
+ * rotation}.  It clobbers the iteration state.  lsq_sell_info: {m, n, nnz, SELL entries of A,
+ * SELL entries of Aᵀ, device bytes of the operator copies}. */
+int lsq_profile_kernels(lsq_handle* h, int32_t reps, double* ms4);
+int lsq_sell_info(lsq_handle* h, int64_t* out6);
+
+/* ---- triangular kernels (replace the Cython kernels; R upper triangular CSR, int32 indices,
+ *      sorted column indices, diagonal first in each row) ------------------------------------ */
+/* spsolve_tr_upper: x = R^-1 b. */
+int tri_upper_solve_csr(int32_t device, int64_t N, const int32_t* indptr, const int32_t* indices,
+                        const double* data, const double* b, double* x);
+/* inv_tr_upper: columns col = N-1..0 of R^-1, entries emitted (col descending, row descending)
+ * when row == col or |x| > tol (tol is a C float, as in the .pyx).  Returns 1 (buffer full)
+ * exactly when inv_tr_upper returns status 1, with the same nnz_max entries in rr/cc/vv (the
+ * last one zero).  *n_out = number of entries written. */
+int tri_upper_inv_csr(int32_t device, int64_t N, const int32_t* indptr, const int32_t* indices,
+                      const double* data, int64_t nnz_max, float tol,
+                      int32_t* rr, int32_t* cc, double* vv, int64_t* n_out);
+/* propagate_qz_errors: E_i = sqrt(sum over columns of (R^-1)_{i,col}^2). */
+int tri_upper_rowrss_csr(int32_t device, int64_t N, const int32_t* indptr, const int32_t* indices,
+                         const double* data, double* E);
+/* Error string of the last failing tri_* call on this thread. */
+const char* tri_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LSQSURF_H */

@@ -1,0 +1,94 @@
+"""ctypes binding of liblsqsurf.so (include/lsqsurf.h).  Product path: there is no fallback —
+if the library is missing or no gfx950 device is present, every call raises."""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'liblsqsurf.so')
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+class LsqOpts(ctypes.Structure):
+    _fields_ = [('method', ctypes.c_int32), ('precond', ctypes.c_int32), ('atol', ctypes.c_double),
+                ('btol', ctypes.c_double), ('conlim', ctypes.c_double), ('maxit', ctypes.c_int64),
+                ('use_x0', ctypes.c_int32), ('batch', ctypes.c_int32), ('use_graph', ctypes.c_int32),
+                ('reserved', ctypes.c_int32)]
+
+
+class LsqStats(ctypes.Structure):
+    _fields_ = [('iters', ctypes.c_int64), ('istop', ctypes.c_int32), ('reserved', ctypes.c_int32),
+                ('r1norm', ctypes.c_double), ('r2norm', ctypes.c_double), ('anorm', ctypes.c_double),
+                ('acond', ctypes.c_double), ('arnorm', ctypes.c_double), ('xnorm', ctypes.c_double),
+                ('time_s', ctypes.c_double), ('bytes_per_iter', ctypes.c_double)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != 'reserved'}
+
+
+# every symbol declared in include/lsqsurf.h
+EXPORTS = ['lsq_default_opts', 'lsq_create', 'lsq_destroy', 'lsq_last_error', 'lsq_set_col_map',
+           'lsq_set_matrix_coo', 'lsq_set_row_weight', 'lsq_set_row_mask', 'lsq_shape', 'lsq_get_csr',
+           'lsq_solve', 'lsq_spmv', 'lsq_iterate', 'lsq_profile_kernels', 'lsq_sell_info',
+           'tri_upper_solve_csr', 'tri_upper_inv_csr', 'tri_upper_rowrss_csr', 'tri_last_error']
+
+_lib = None
+
+
+def load():
+    """Load liblsqsurf.so (in-tree build).  Raises NativeError if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(f'{LIB_PATH} not built: run `python -m lssurf_amd.build` (hipcc, gfx950)')
+    L = ctypes.CDLL(LIB_PATH)
+    P, i32, i64, f64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+    sig = {
+        'lsq_default_opts': ([P], None),
+        'lsq_create': ([i32], P),
+        'lsq_destroy': ([P], None),
+        'lsq_last_error': ([P], ctypes.c_char_p),
+        'lsq_set_col_map': ([P, i64, P, i64], ctypes.c_int),
+        'lsq_set_matrix_coo': ([P, i64, i64, i64, P, P, P, P], ctypes.c_int),
+        'lsq_set_row_weight': ([P, P], ctypes.c_int),
+        'lsq_set_row_mask': ([P, P], ctypes.c_int),
+        'lsq_shape': ([P, P, P, P], ctypes.c_int),
+        'lsq_get_csr': ([P, P, P, P], ctypes.c_int),
+        'lsq_solve': ([P, P, P, P, P], ctypes.c_int),
+        'lsq_spmv': ([P, i32, P, P], ctypes.c_int),
+        'lsq_iterate': ([P, P, i64, P, P], ctypes.c_int),
+        'lsq_profile_kernels': ([P, i32, P], ctypes.c_int),
+        'lsq_sell_info': ([P, P], ctypes.c_int),
+        'tri_upper_solve_csr': ([i32, i64, P, P, P, P, P], ctypes.c_int),
+        'tri_upper_inv_csr': ([i32, i64, P, P, P, i64, ctypes.c_float, P, P, P, P], ctypes.c_int),
+        'tri_upper_rowrss_csr': ([i32, i64, P, P, P, P], ctypes.c_int),
+        'tri_last_error': ([], ctypes.c_char_p),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def as_c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+def default_opts(**kw):
+    o = LsqOpts()
+    load().lsq_default_opts(ctypes.byref(o))
+    for k, v in kw.items():
+        if v is not None:
+            setattr(o, k, v)
+    return o

@@ -1,0 +1,264 @@
+// api.hip — extern "C" entry points of liblsqsurf.so (declared in include/lsqsurf.h).
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "../../include/lsqsurf.h"
+#include "system.hpp"
+
+namespace lsq {
+void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts& o, bool no_stop);
+int lsqr_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq_stats* stats);
+int lsqr_iterate(System& S, const double* h_b, int64_t iters, const lsq_opts& o, lsq_stats* stats);
+void lsqr_profile(System& S, int reps, double* ms_out);
+void graph_cache_drop(const System* S);
+}  // namespace lsq
+
+struct lsq_handle {
+    lsq::System sys;
+};
+
+namespace {
+
+template <class F>
+int guarded(lsq_handle* h, F&& f) {
+    if (!h) return -1;
+    h->sys.err.clear();
+    try {
+        HIP_CHECK(hipSetDevice(h->sys.device));
+        return f(h->sys);
+    } catch (const std::invalid_argument& e) {
+        h->sys.err = e.what();
+        return -2;
+    } catch (const std::exception& e) {
+        h->sys.err = e.what();
+        return -3;
+    }
+}
+
+int fail(lsq::System& S, const std::string& msg) {
+    S.err = msg;
+    return -2;
+}
+
+}  // namespace
+
+extern "C" {
+
+void lsq_default_opts(lsq_opts* o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof(*o));
+    o->method = 0;
+    o->precond = 1;
+    o->atol = 1e-10;
+    o->btol = 1e-10;
+    o->conlim = 1e8;
+    o->maxit = 0;   // 0 -> 4 n
+    o->use_x0 = 0;
+    o->batch = 16;
+    o->use_graph = 1;
+}
+
+lsq_handle* lsq_create(int32_t device) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) return nullptr;
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return nullptr;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return nullptr;   // gfx950 code objects only
+    auto* h = new lsq_handle();
+    h->sys.device = device;
+    if (hipStreamCreateWithFlags(&h->sys.stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return nullptr;
+    }
+    return h;
+}
+
+void lsq_destroy(lsq_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->sys.device);
+    lsq::graph_cache_drop(&h->sys);
+    (void)hipStreamSynchronize(h->sys.stream);
+    delete h;
+}
+
+const char* lsq_last_error(lsq_handle* h) { return h ? h->sys.err.c_str() : "null handle"; }
+
+int lsq_set_col_map(lsq_handle* h, int64_t n_full, const int64_t* keep_cols, int64_t n_keep) {
+    return guarded(h, [&](lsq::System& S) {
+        if (S.G.rp.p) return fail(S, "lsq_set_col_map must precede lsq_set_matrix_coo");
+        if (n_full <= 0 || n_keep < 0 || n_keep > n_full || (n_keep && !keep_cols))
+            return fail(S, "lsq_set_col_map: bad sizes");
+        std::vector<int32_t> map(n_full, -1);
+        for (int64_t k = 0; k < n_keep; ++k) {
+            const int64_t c = keep_cols[k];
+            if (c < 0 || c >= n_full || (k && c <= keep_cols[k - 1]))
+                return fail(S, "lsq_set_col_map: keep_cols must be strictly increasing in [0, n_full)");
+            map[c] = (int32_t)k;
+        }
+        S.colmap.alloc(n_full);
+        S.colmap.upload(map.data(), n_full, S.stream);
+        HIP_CHECK(hipStreamSynchronize(S.stream));
+        S.n_full = n_full;
+        S.n_keep = n_keep;
+        S.have_colmap = true;
+        return 0;
+    });
+}
+
+int lsq_set_matrix_coo(lsq_handle* h, int64_t m, int64_t n_full, int64_t nnz, const int64_t* r, const int64_t* c,
+                       const double* v, const double* row_weight) {
+    return guarded(h, [&](lsq::System& S) {
+        if (m <= 0 || n_full <= 0 || nnz < 0 || (nnz && (!r || !c || !v)))
+            return fail(S, "lsq_set_matrix_coo: bad arguments");
+        if (S.have_colmap && n_full != S.n_full) return fail(S, "lsq_set_matrix_coo: n_full differs from col map");
+        if (m >= (int64_t)INT32_MAX || n_full >= (int64_t)INT32_MAX)
+            return fail(S, "lsq_set_matrix_coo: dimensions must fit int32 column indices");
+        if (S.G.rp.p) return fail(S, "lsq_set_matrix_coo: matrix already set (create a new handle)");
+        lsq::graph_cache_drop(&S);
+        lsq::form_from_coo(S, m, n_full, nnz, r, c, v);
+        if (row_weight) {
+            S.roww.upload(row_weight, m, S.stream);
+            HIP_CHECK(hipStreamSynchronize(S.stream));
+        }
+        return 0;
+    });
+}
+
+int lsq_set_row_weight(lsq_handle* h, const double* row_weight) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_set_row_weight: no matrix");
+        if (row_weight) {
+            S.roww.upload(row_weight, S.G.m, S.stream);
+        } else {
+            std::vector<double> one(S.G.m, 1.0);
+            S.roww.upload(one.data(), S.G.m, S.stream);
+        }
+        HIP_CHECK(hipStreamSynchronize(S.stream));
+        S.rs_dirty = true;
+        return 0;
+    });
+}
+
+int lsq_set_row_mask(lsq_handle* h, const uint8_t* keep) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_set_row_mask: no matrix");
+        if (keep) {
+            std::vector<uint8_t> k(keep, keep + S.G.m);
+            for (auto& x : k) x = x ? 1 : 0;
+            S.rowkeep.upload(k.data(), S.G.m, S.stream);
+        } else {
+            HIP_CHECK(hipMemsetAsync(S.rowkeep.p, 1, S.G.m, S.stream));
+        }
+        HIP_CHECK(hipStreamSynchronize(S.stream));
+        S.rs_dirty = true;
+        return 0;
+    });
+}
+
+int lsq_shape(lsq_handle* h, int64_t* m, int64_t* n, int64_t* nnz) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_shape: no matrix");
+        std::vector<int64_t> rp(S.G.m + 1);
+        std::vector<uint8_t> keep(S.G.m);
+        S.G.rp.download(rp.data(), S.G.m + 1, S.stream);
+        S.rowkeep.download(keep.data(), S.G.m, S.stream);
+        HIP_CHECK(hipStreamSynchronize(S.stream));
+        int64_t mk = 0, zk = 0;
+        for (int64_t i = 0; i < S.G.m; ++i)
+            if (keep[i]) { ++mk; zk += rp[i + 1] - rp[i]; }
+        if (m) *m = mk;
+        if (n) *n = S.G.n;
+        if (nnz) *nnz = zk;
+        return 0;
+    });
+}
+
+int lsq_get_csr(lsq_handle* h, int64_t* indptr, int32_t* indices, double* data) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_get_csr: no matrix");
+        const int64_t m = S.G.m, z = S.G.nnz;
+        std::vector<int64_t> rp(m + 1);
+        std::vector<int32_t> ci(std::max<int64_t>(z, 1));
+        std::vector<double> val(std::max<int64_t>(z, 1)), rw(m);
+        std::vector<uint8_t> keep(m);
+        S.G.rp.download(rp.data(), m + 1, S.stream);
+        S.G.ci.download(ci.data(), z, S.stream);
+        S.G.val.download(val.data(), z, S.stream);
+        S.roww.download(rw.data(), m, S.stream);
+        S.rowkeep.download(keep.data(), m, S.stream);
+        HIP_CHECK(hipStreamSynchronize(S.stream));
+        int64_t o = 0, r = 0;
+        indptr[0] = 0;
+        for (int64_t i = 0; i < m; ++i) {
+            if (!keep[i]) continue;
+            for (int64_t e = rp[i]; e < rp[i + 1]; ++e) {
+                indices[o] = ci[e];
+                data[o] = val[e] * rw[i];   // = TCinv·G entry, the single IEEE product the reference forms
+                ++o;
+            }
+            indptr[++r] = o;
+        }
+        return 0;
+    });
+}
+
+int lsq_solve(lsq_handle* h, const double* b, double* x_inout, const lsq_opts* o, lsq_stats* s) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_solve: no matrix");
+        if (!b || !x_inout) return fail(S, "lsq_solve: null b or x");
+        lsq_opts d;
+        lsq_default_opts(&d);
+        if (!o) o = &d;
+        if (o->method != 0) return fail(S, "lsq_solve: only method 0 (LSQR) is implemented");
+        if (o->precond < 0 || o->precond > 1) return fail(S, "lsq_solve: precond must be 0 or 1");
+        return lsq::lsqr_solve(S, b, x_inout, *o, s);
+    });
+}
+
+int lsq_iterate(lsq_handle* h, const double* b, int64_t iters, const lsq_opts* o, lsq_stats* s) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_iterate: no matrix");
+        lsq_opts d;
+        lsq_default_opts(&d);
+        if (!o) o = &d;
+        return lsq::lsqr_iterate(S, b, iters, *o, s);
+    });
+}
+
+int lsq_profile_kernels(lsq_handle* h, int32_t reps, double* ms4) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_profile_kernels: no matrix");
+        lsq::lsqr_profile(S, reps > 0 ? reps : 10, ms4);
+        return 0;
+    });
+}
+
+int lsq_sell_info(lsq_handle* h, int64_t* out6) {
+    return guarded(h, [&](lsq::System& S) {
+        out6[0] = S.G.m;
+        out6[1] = S.G.n;
+        out6[2] = S.G.nnz;
+        out6[3] = S.A.nent;
+        out6[4] = S.AT.nent;
+        out6[5] = (int64_t)(S.G.rp.bytes() + S.G.ci.bytes() + S.G.val.bytes() + S.GT.rp.bytes() + S.GT.ci.bytes() +
+                            S.GT.val.bytes() + S.A.ci.bytes() + S.A.val.bytes() + S.AT.ci.bytes() + S.AT.val.bytes());
+        return 0;
+    });
+}
+
+int lsq_spmv(lsq_handle* h, int32_t trans, const double* x, double* y) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_spmv: no matrix");
+        const int64_t nin = trans ? S.G.m : S.G.n, nout = trans ? S.G.n : S.G.m;
+        lsq::DBuf<double> dx(std::max<int64_t>(nin, 1)), dy(std::max<int64_t>(nout, 1));
+        dx.upload(x, nin, S.stream);
+        lsq::csr_spmv(S, trans ? 1 : 0, dx.p, dy.p);
+        dy.download(y, nout, S.stream);
+        HIP_CHECK(hipStreamSynchronize(S.stream));
+        return 0;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,422 @@
+// build.hip — device formation of the least-squares operator (replaces the scipy assembly of
+// LSsurf/smooth_fit.py:613-627 and lin_op.toCSR, lin_op.py:745-753).
+//
+//   COO (r, c, v) ──drop v==0, Ip_c──▶ row buckets ──sort (col, input order), sum duplicates,
+//   drop zero sums──▶ canonical CSR G ──▶ transpose GT ──▶ SELL-64 copies A, AT with values
+//   diag(rs)·G·diag(cs).
+//
+// Everything is integer bookkeeping plus one f64 add per duplicate, so the formed G is
+// bit-identical to scipy's for any input whose duplicates are at most pairs (the smooth_fit
+// systems have none); see DESIGN.md §Formation.
+#include <algorithm>
+#include <vector>
+
+#include "system.hpp"
+
+namespace lsq {
+
+namespace {
+
+constexpr int64_t MAX_SEG = 1 << 16;   // longest row / column handled by the per-segment sort
+
+struct BuildErr {
+    unsigned long long count;
+    long long first;      // first offending COO index
+    int kind;             // 1 row out of range, 2 col out of range, 3 segment too long
+};
+
+__global__ __launch_bounds__(BLOCK) void k_coo_count(int64_t nnz, int64_t m, int64_t n_full,
+                                                     const int64_t* __restrict__ r,
+                                                     const int64_t* __restrict__ c,
+                                                     const double* __restrict__ v,
+                                                     const int32_t* __restrict__ colmap,
+                                                     unsigned long long* __restrict__ cnt,
+                                                     BuildErr* err) {
+    for (int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x; e < nnz; e += (int64_t)gridDim.x * BLOCK) {
+        if (v[e] == 0.0) continue;                      // lin_op.toCSR: good = v != 0
+        const int64_t ri = r[e], cj = c[e];
+        int kind = 0;
+        if (ri < 0 || ri >= m) kind = 1;
+        else if (cj < 0 || cj >= n_full) kind = 2;
+        if (kind) {
+            if (atomicAdd(&err->count, 1ull) == 0) { err->first = e; err->kind = kind; }
+            continue;
+        }
+        if (colmap && colmap[cj] < 0) continue;         // column removed by Ip_c
+        atomicAdd(&cnt[ri], 1ull);
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_coo_scatter(int64_t nnz, const int64_t* __restrict__ r,
+                                                       const int64_t* __restrict__ c,
+                                                       const double* __restrict__ v,
+                                                       const int32_t* __restrict__ colmap,
+                                                       const int64_t* __restrict__ off,
+                                                       unsigned long long* __restrict__ cur,
+                                                       int32_t* __restrict__ tc, double* __restrict__ tv,
+                                                       int64_t* __restrict__ te) {
+    for (int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x; e < nnz; e += (int64_t)gridDim.x * BLOCK) {
+        const double ve = v[e];
+        if (ve == 0.0) continue;
+        const int64_t ri = r[e];
+        int64_t cj = c[e];
+        if (colmap) {
+            cj = colmap[cj];
+            if (cj < 0) continue;
+        }
+        const int64_t pos = off[ri] + (int64_t)atomicAdd(&cur[ri], 1ull);
+        tc[pos] = (int32_t)cj;
+        tv[pos] = ve;
+        te[pos] = e;
+    }
+}
+
+// One thread per row: insertion sort by (col, input index), then sum duplicates in input
+// order and drop zero sums; the deduplicated entries are written to the segment's front.
+__global__ __launch_bounds__(BLOCK) void k_row_sort_dedupe(int64_t m, const int64_t* __restrict__ off,
+                                                           int32_t* __restrict__ tc, double* __restrict__ tv,
+                                                           int64_t* __restrict__ te,
+                                                           int64_t* __restrict__ dcnt, BuildErr* err) {
+    for (int64_t row = (int64_t)blockIdx.x * BLOCK + threadIdx.x; row < m; row += (int64_t)gridDim.x * BLOCK) {
+        const int64_t b = off[row], L = off[row + 1] - b;
+        if (L > MAX_SEG) {
+            if (atomicAdd(&err->count, 1ull) == 0) { err->first = row; err->kind = 3; }
+            dcnt[row] = 0;
+            continue;
+        }
+        for (int64_t i = 1; i < L; ++i) {
+            const int32_t kc = tc[b + i];
+            const double kv = tv[b + i];
+            const int64_t ke = te[b + i];
+            int64_t j = i - 1;
+            while (j >= 0 && (tc[b + j] > kc || (tc[b + j] == kc && te[b + j] > ke))) {
+                tc[b + j + 1] = tc[b + j];
+                tv[b + j + 1] = tv[b + j];
+                te[b + j + 1] = te[b + j];
+                --j;
+            }
+            tc[b + j + 1] = kc;
+            tv[b + j + 1] = kv;
+            te[b + j + 1] = ke;
+        }
+        int64_t out = 0;
+        int64_t i = 0;
+        while (i < L) {
+            const int32_t col = tc[b + i];
+            double s = tv[b + i];
+            int64_t k = i + 1;
+            while (k < L && tc[b + k] == col) { s += tv[b + k]; ++k; }
+            if (s != 0.0) {                     // scipy csr_matmat drops zero sums
+                tc[b + out] = col;
+                tv[b + out] = s;
+                ++out;
+            }
+            i = k;
+        }
+        dcnt[row] = out;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_compact(int64_t m, const int64_t* __restrict__ off,
+                                                   const int32_t* __restrict__ tc, const double* __restrict__ tv,
+                                                   const int64_t* __restrict__ rp, int32_t* __restrict__ ci,
+                                                   double* __restrict__ val) {
+    for (int64_t row = (int64_t)blockIdx.x * BLOCK + threadIdx.x; row < m; row += (int64_t)gridDim.x * BLOCK) {
+        const int64_t b = off[row], o = rp[row], L = rp[row + 1] - o;
+        for (int64_t k = 0; k < L; ++k) {
+            ci[o + k] = tc[b + k];
+            val[o + k] = tv[b + k];
+        }
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_u64_to_i64(int64_t n, const unsigned long long* __restrict__ a,
+                                                      int64_t* __restrict__ b) {
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK)
+        b[i] = (int64_t)a[i];
+}
+
+// ---- transpose -------------------------------------------------------------------------------
+__global__ __launch_bounds__(BLOCK) void k_col_count(int64_t m, const int64_t* __restrict__ rp,
+                                                     const int32_t* __restrict__ ci,
+                                                     unsigned long long* __restrict__ cnt) {
+    for (int64_t row = (int64_t)blockIdx.x * BLOCK + threadIdx.x; row < m; row += (int64_t)gridDim.x * BLOCK)
+        for (int64_t e = rp[row]; e < rp[row + 1]; ++e) atomicAdd(&cnt[ci[e]], 1ull);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_t_scatter(int64_t m, const int64_t* __restrict__ rp,
+                                                     const int32_t* __restrict__ ci, const double* __restrict__ val,
+                                                     const int64_t* __restrict__ trp,
+                                                     unsigned long long* __restrict__ cur,
+                                                     int32_t* __restrict__ tci, double* __restrict__ tval) {
+    for (int64_t row = (int64_t)blockIdx.x * BLOCK + threadIdx.x; row < m; row += (int64_t)gridDim.x * BLOCK)
+        for (int64_t e = rp[row]; e < rp[row + 1]; ++e) {
+            const int32_t j = ci[e];
+            const int64_t pos = trp[j] + (int64_t)atomicAdd(&cur[j], 1ull);
+            tci[pos] = (int32_t)row;
+            tval[pos] = val[e];
+        }
+}
+
+// Column segments: sort by row index (unique within a column) -> deterministic GT.
+__global__ __launch_bounds__(BLOCK) void k_seg_sort(int64_t n, const int64_t* __restrict__ rp,
+                                                    int32_t* __restrict__ ci, double* __restrict__ val,
+                                                    BuildErr* err) {
+    for (int64_t row = (int64_t)blockIdx.x * BLOCK + threadIdx.x; row < n; row += (int64_t)gridDim.x * BLOCK) {
+        const int64_t b = rp[row], L = rp[row + 1] - b;
+        if (L > MAX_SEG) {
+            if (atomicAdd(&err->count, 1ull) == 0) { err->first = row; err->kind = 3; }
+            continue;
+        }
+        for (int64_t i = 1; i < L; ++i) {
+            const int32_t kc = ci[b + i];
+            const double kv = val[b + i];
+            int64_t j = i - 1;
+            while (j >= 0 && ci[b + j] > kc) {
+                ci[b + j + 1] = ci[b + j];
+                val[b + j + 1] = val[b + j];
+                --j;
+            }
+            ci[b + j + 1] = kc;
+            val[b + j + 1] = kv;
+        }
+    }
+}
+
+// ---- SELL-64 ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(BLOCK) void k_slice_width(int64_t rows, int64_t nslices,
+                                                       const int64_t* __restrict__ rp,
+                                                       int64_t* __restrict__ wid) {
+    for (int64_t s = (int64_t)blockIdx.x * BLOCK + threadIdx.x; s < nslices; s += (int64_t)gridDim.x * BLOCK) {
+        int64_t w = 0;
+        const int64_t r0 = s * SELL_C;
+        const int64_t r1 = r0 + SELL_C < rows ? r0 + SELL_C : rows;
+        for (int64_t r = r0; r < r1; ++r) w = max(w, rp[r + 1] - rp[r]);
+        wid[s] = w * SELL_C;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_sell_cols(int64_t rows, const int64_t* __restrict__ rp,
+                                                     const int32_t* __restrict__ ci,
+                                                     const int64_t* __restrict__ sp, int32_t* __restrict__ sci) {
+    for (int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BLOCK) {
+        const int64_t s = r / SELL_C, lane = r % SELL_C;
+        const int64_t base = sp[s], W = (sp[s + 1] - base) / SELL_C;
+        const int64_t b = rp[r], L = rp[r + 1] - b;
+        const int32_t padc = L ? ci[b + L - 1] : 0;
+        for (int64_t k = 0; k < W; ++k) sci[base + k * SELL_C + lane] = k < L ? ci[b + k] : padc;
+    }
+}
+
+// val_sell = (g * rs[row]) * cs[col]; `rowsc`/`colsc` index by the CSR's own row / column ids.
+__global__ __launch_bounds__(BLOCK) void k_sell_vals(int64_t rows, const int64_t* __restrict__ rp,
+                                                     const int32_t* __restrict__ ci, const double* __restrict__ g,
+                                                     const double* __restrict__ rowsc,
+                                                     const double* __restrict__ colsc, int transposed,
+                                                     const int64_t* __restrict__ sp, double* __restrict__ sval) {
+    for (int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BLOCK) {
+        const int64_t s = r / SELL_C, lane = r % SELL_C;
+        const int64_t base = sp[s], W = (sp[s + 1] - base) / SELL_C;
+        const int64_t b = rp[r], L = rp[r + 1] - b;
+        for (int64_t k = 0; k < W; ++k) {
+            double x = 0.0;
+            if (k < L) {
+                const int32_t c = ci[b + k];
+                // A: row scale of r, col scale of c.  AT: row scale of c, col scale of r.
+                x = transposed ? (g[b + k] * rowsc[c]) * colsc[r] : (g[b + k] * rowsc[r]) * colsc[c];
+            }
+            sval[base + k * SELL_C + lane] = x;
+        }
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_rowscale(int64_t m, const double* __restrict__ w,
+                                                    const uint8_t* __restrict__ keep, double* __restrict__ rs) {
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += (int64_t)gridDim.x * BLOCK)
+        rs[i] = keep[i] ? w[i] : 0.0;
+}
+
+// Jacobi column scaling: cs_j = 1/||(diag(rs) G)_{:,j}||  (1 for an empty column).
+__global__ __launch_bounds__(BLOCK) void k_colnorm(int64_t n, const int64_t* __restrict__ trp,
+                                                   const int32_t* __restrict__ tci, const double* __restrict__ tval,
+                                                   const double* __restrict__ rs, double* __restrict__ cs) {
+    for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLOCK) {
+        double s = 0.0;
+        for (int64_t e = trp[j]; e < trp[j + 1]; ++e) {
+            const double a = tval[e] * rs[tci[e]];
+            s += a * a;
+        }
+        cs[j] = s > 0.0 ? 1.0 / sqrt(s) : 1.0;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_fill(int64_t n, double v, double* __restrict__ a) {
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) a[i] = v;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_csr_spmv(int64_t rows, const int64_t* __restrict__ rp,
+                                                    const int32_t* __restrict__ ci, const double* __restrict__ val,
+                                                    const double* __restrict__ x, double* __restrict__ y) {
+    for (int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BLOCK) {
+        double acc = 0.0;
+        for (int64_t e = rp[r]; e < rp[r + 1]; ++e) acc += val[e] * x[ci[e]];
+        y[r] = acc;
+    }
+}
+
+void check_err(BuildErr* d_err, hipStream_t s, const char* stage) {
+    BuildErr h{};
+    HIP_CHECK(hipMemcpyAsync(&h, d_err, sizeof(BuildErr), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (h.count) {
+        const char* what = h.kind == 1 ? "row index out of range" : h.kind == 2 ? "column index out of range"
+                                                                                : "segment longer than 65536 entries";
+        throw std::invalid_argument(std::string(stage) + ": " + what + " (first at " + std::to_string(h.first) +
+                                    ", " + std::to_string(h.count) + " total)");
+    }
+}
+
+void build_sell(Sell& S, const Csr& C, hipStream_t st) {
+    S.rows = C.m;
+    S.nslices = (C.m + SELL_C - 1) / SELL_C;
+    S.sp.alloc(S.nslices + 1);
+    S.sp.zero(st);
+    hipLaunchKernelGGL(k_slice_width, dim3(grid_for(S.nslices)), dim3(BLOCK), 0, st, C.m, S.nslices, C.rp.p, S.sp.p);
+    KERNEL_CHECK();
+    S.nent = exclusive_scan_i64(S.sp.p, S.nslices + 1, st);
+    S.ci.alloc(std::max<int64_t>(S.nent, 1));
+    S.val.alloc(std::max<int64_t>(S.nent, 1));
+    hipLaunchKernelGGL(k_sell_cols, dim3(grid_for(C.m)), dim3(BLOCK), 0, st, C.m, C.rp.p, C.ci.p, S.sp.p, S.ci.p);
+    KERNEL_CHECK();
+}
+
+}  // namespace
+
+void form_from_coo(System& S, int64_t m, int64_t n_full, int64_t nnz, const int64_t* r, const int64_t* c,
+                   const double* v) {
+    hipStream_t st = S.stream;
+    const int64_t n = S.have_colmap ? S.n_keep : n_full;   // compact width (lsq_set_col_map)
+    DBuf<int64_t> dr(nnz), dc(nnz);
+    DBuf<double> dv(nnz);
+    dr.upload(r, nnz, st);
+    dc.upload(c, nnz, st);
+    dv.upload(v, nnz, st);
+    DBuf<BuildErr> err(1);
+    err.zero(st);
+    DBuf<unsigned long long> cnt(m + 1), cur(m + 1);
+    cnt.zero(st);
+    cur.zero(st);
+    const int32_t* cmap = S.have_colmap ? S.colmap.p : nullptr;
+    const int gE = grid_for(nnz);
+    hipLaunchKernelGGL(k_coo_count, dim3(gE), dim3(BLOCK), 0, st, nnz, m, n_full, dr.p, dc.p, dv.p, cmap, cnt.p, err.p);
+    KERNEL_CHECK();
+    check_err(err.p, st, "lsq_set_matrix_coo");
+    DBuf<int64_t> off(m + 1);
+    hipLaunchKernelGGL(k_u64_to_i64, dim3(grid_for(m + 1)), dim3(BLOCK), 0, st, m + 1, cnt.p, off.p);
+    KERNEL_CHECK();
+    const int64_t kept = exclusive_scan_i64(off.p, m + 1, st);
+    DBuf<int32_t> tc(std::max<int64_t>(kept, 1));
+    DBuf<double> tv(std::max<int64_t>(kept, 1));
+    DBuf<int64_t> te(std::max<int64_t>(kept, 1));
+    hipLaunchKernelGGL(k_coo_scatter, dim3(gE), dim3(BLOCK), 0, st, nnz, dr.p, dc.p, dv.p, cmap, off.p, cur.p, tc.p,
+                       tv.p, te.p);
+    KERNEL_CHECK();
+    dr.release();
+    dc.release();
+    dv.release();
+    DBuf<int64_t> dcnt(m + 1);
+    dcnt.zero(st);
+    hipLaunchKernelGGL(k_row_sort_dedupe, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, off.p, tc.p, tv.p, te.p, dcnt.p,
+                       err.p);
+    KERNEL_CHECK();
+    check_err(err.p, st, "lsq_set_matrix_coo");
+    te.release();
+
+    Csr& G = S.G;
+    G.m = m;
+    G.n = n;
+    G.rp = std::move(dcnt);
+    G.nnz = exclusive_scan_i64(G.rp.p, m + 1, st);
+    G.ci.alloc(std::max<int64_t>(G.nnz, 1));
+    G.val.alloc(std::max<int64_t>(G.nnz, 1));
+    hipLaunchKernelGGL(k_compact, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, off.p, tc.p, tv.p, G.rp.p, G.ci.p, G.val.p);
+    KERNEL_CHECK();
+    tc.release();
+    tv.release();
+    off.release();
+
+    // transpose
+    Csr& T = S.GT;
+    T.m = n;
+    T.n = m;
+    T.nnz = G.nnz;
+    DBuf<unsigned long long> ccnt(n + 1), ccur(n + 1);
+    ccnt.zero(st);
+    ccur.zero(st);
+    hipLaunchKernelGGL(k_col_count, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, G.rp.p, G.ci.p, ccnt.p);
+    KERNEL_CHECK();
+    T.rp.alloc(n + 1);
+    hipLaunchKernelGGL(k_u64_to_i64, dim3(grid_for(n + 1)), dim3(BLOCK), 0, st, n + 1, ccnt.p, T.rp.p);
+    KERNEL_CHECK();
+    exclusive_scan_i64(T.rp.p, n + 1, st);
+    T.ci.alloc(std::max<int64_t>(T.nnz, 1));
+    T.val.alloc(std::max<int64_t>(T.nnz, 1));
+    hipLaunchKernelGGL(k_t_scatter, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, G.rp.p, G.ci.p, G.val.p, T.rp.p, ccur.p,
+                       T.ci.p, T.val.p);
+    KERNEL_CHECK();
+    hipLaunchKernelGGL(k_seg_sort, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, T.rp.p, T.ci.p, T.val.p, err.p);
+    KERNEL_CHECK();
+    check_err(err.p, st, "lsq_set_matrix_coo (transpose)");
+
+    build_sell(S.A, G, st);
+    build_sell(S.AT, T, st);
+
+    // default scaling state: weights 1, all rows kept, no preconditioner
+    S.roww.alloc(m);
+    hipLaunchKernelGGL(k_fill, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, 1.0, S.roww.p);
+    KERNEL_CHECK();
+    S.rowkeep.alloc(m);
+    HIP_CHECK(hipMemsetAsync(S.rowkeep.p, 1, m, st));
+    S.rs.alloc(m);
+    S.cs.alloc(std::max<int64_t>(n, 1));
+    S.rs_dirty = true;
+    S.cs_mode = -1;
+    S.iter_ready = false;
+    HIP_CHECK(hipStreamSynchronize(st));
+}
+
+void refresh_scaling(System& S, int precond) {
+    hipStream_t st = S.stream;
+    const int64_t m = S.G.m, n = S.G.n;
+    if (!S.rs_dirty && S.cs_mode == precond) return;
+    hipLaunchKernelGGL(k_rowscale, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, S.roww.p, S.rowkeep.p, S.rs.p);
+    KERNEL_CHECK();
+    if (precond == 1) {
+        hipLaunchKernelGGL(k_colnorm, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, S.GT.rp.p, S.GT.ci.p, S.GT.val.p,
+                           S.rs.p, S.cs.p);
+    } else {
+        hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, 1.0, S.cs.p);
+    }
+    KERNEL_CHECK();
+    hipLaunchKernelGGL(k_sell_vals, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, S.G.rp.p, S.G.ci.p, S.G.val.p, S.rs.p,
+                       S.cs.p, 0, S.A.sp.p, S.A.val.p);
+    KERNEL_CHECK();
+    hipLaunchKernelGGL(k_sell_vals, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, S.GT.rp.p, S.GT.ci.p, S.GT.val.p, S.rs.p,
+                       S.cs.p, 1, S.AT.sp.p, S.AT.val.p);
+    KERNEL_CHECK();
+    S.rs_dirty = false;
+    S.cs_mode = precond;
+    S.iter_ready = false;
+}
+
+void csr_spmv(System& S, int trans, const double* dx, double* dy) {
+    const Csr& C = trans ? S.GT : S.G;
+    hipLaunchKernelGGL(k_csr_spmv, dim3(grid_for(C.m)), dim3(BLOCK), 0, S.stream, C.m, C.rp.p, C.ci.p, C.val.p, dx, dy);
+    KERNEL_CHECK();
+}
+
+System::~System() {
+    if (stream) (void)hipStreamDestroy(stream);
+}
+
+}  // namespace lsq

@@ -1,0 +1,588 @@
+// lsqr.hip — LSQR (Paige & Saunders 1982; scipy.sparse.linalg.lsqr's recurrences and stopping
+// rules) on the device-resident SELL-64 system.  Replaces sparseqr.solve at
+// LSsurf/smooth_fit.py:142.
+//
+// One iteration = four launches, all scalars stay on the device (no host round trip):
+//   k_xw_spmv   [x/w update of the previous iteration  ‖  u ← (A ṽ)/α − α ũ/β ] + Σu², Σw²
+//   k_beta      β = ‖u‖, ‖A‖ update                          (1 block, deterministic reduce)
+//   k_spmtv     ṽ' ← (Aᵀ ũ)/β − β ṽ/α                         + Σṽ'²
+//   k_givens    α = ‖ṽ'‖, plane rotation, norms, stopping test (1 block)
+// ũ and ṽ are kept UNNORMALISED; the 1/β and 1/α scalings are folded into the next product,
+// so normalisation costs no extra pass over HBM.  ṽ ping-pongs between two buffers.  Batches
+// of iterations are captured once into a hipGraph and replayed; the host reads the 200-byte
+// state only between batches.  Right preconditioning by column scaling is baked into the SELL
+// values (A·D), and x = D y is applied on the way out.
+#include <chrono>
+#include <cmath>
+#include <vector>
+
+#include "system.hpp"
+#include "../../include/lsqsurf.h"
+
+namespace lsq {
+
+namespace {
+
+constexpr int NPART = 2048;   // partial-sum slots per reduction (fixed grid => deterministic)
+
+// ---- SELL-64 row kernel body: one lane = one row, 4 entries in flight per step -------------
+__device__ __forceinline__ double sell_row_dot(const int32_t* __restrict__ ci, const double* __restrict__ val,
+                                               int64_t base, int64_t W, int lane,
+                                               const double* __restrict__ x) {
+    const int32_t* c = ci + base + lane;
+    const double* v = val + base + lane;
+    double a0 = 0.0, a1 = 0.0;
+    int64_t k = 0;
+    for (; k + 4 <= W; k += 4) {
+        const int32_t c0 = c[(k + 0) * SELL_C], c1 = c[(k + 1) * SELL_C];
+        const int32_t c2 = c[(k + 2) * SELL_C], c3 = c[(k + 3) * SELL_C];
+        const double v0 = v[(k + 0) * SELL_C], v1 = v[(k + 1) * SELL_C];
+        const double v2 = v[(k + 2) * SELL_C], v3 = v[(k + 3) * SELL_C];
+        a0 += v0 * x[c0];
+        a1 += v1 * x[c1];
+        a0 += v2 * x[c2];
+        a1 += v3 * x[c3];
+    }
+    for (; k < W; ++k) a0 += v[k * SELL_C] * x[c[k * SELL_C]];
+    return a0 + a1;
+}
+
+// partial-sum epilogue: one value per block into part[blockIdx-relative slot]
+__device__ __forceinline__ void store_partial(double acc, double* part, int slot) {
+    __shared__ double red[4];
+    const double s = block_sum(acc, red);
+    if (threadIdx.x == 0) part[slot] = s;
+}
+
+// ---- init: u = rs∘b − A y0 ; partials Σu², Σ(rs∘b)² -----------------------------------------
+__global__ __launch_bounds__(BLOCK) void k_init_u(int64_t m, int64_t nslices, const int64_t* __restrict__ sp,
+                                                  const int32_t* __restrict__ ci, const double* __restrict__ val,
+                                                  const double* __restrict__ rs, const double* __restrict__ b,
+                                                  const double* __restrict__ y0, double* __restrict__ u,
+                                                  double* __restrict__ bw, double* part_u, double* part_b) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double su = 0.0, sb = 0.0;
+    for (int64_t s = (int64_t)blockIdx.x * 4 + wid; s < nslices; s += (int64_t)gridDim.x * 4) {
+        const int64_t row = s * SELL_C + lane;
+        double ax = 0.0;
+        if (y0) {
+            const int64_t base = sp[s];
+            ax = sell_row_dot(ci, val, base, (sp[s + 1] - base) / SELL_C, lane, y0);
+        }
+        if (row < m) {
+            const double bb = rs[row] * b[row];
+            const double uu = bb - ax;
+            bw[row] = bb;
+            u[row] = uu;
+            su += uu * uu;
+            sb += bb * bb;
+        }
+    }
+    store_partial(su, part_u, blockIdx.x);
+    store_partial(sb, part_b, blockIdx.x);
+}
+
+// ---- merged: x/w update (blocks [0,gX)) ‖ SpMV u-update (blocks [gX, gX+gA)) ----------------
+__global__ __launch_bounds__(BLOCK) void k_xw_spmv(const LsqState* __restrict__ st, int gX,
+                                                   int64_t n, double* __restrict__ y, double* __restrict__ w,
+                                                   const double* __restrict__ vt, int64_t m, int64_t nslices,
+                                                   const int64_t* __restrict__ sp, const int32_t* __restrict__ ci,
+                                                   const double* __restrict__ val, double* __restrict__ u,
+                                                   double* part_u, double* part_w) {
+    if ((int)blockIdx.x < gX) {
+        // x/w update for the iteration whose rotation k_givens just finished
+        if (st->finished || !st->have_xw) return;
+        const double t1 = st->t1, t2 = st->t2, ia = st->inv_alpha;
+        double sw = 0.0;
+        for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (int64_t)gX * BLOCK) {
+            const double wj = w[j];
+            y[j] += t1 * wj;
+            const double wn = vt[j] * ia + t2 * wj;
+            w[j] = wn;
+            sw += wn * wn;
+        }
+        store_partial(sw, part_w, blockIdx.x);
+        return;
+    }
+    if (st->stop) return;
+    const int bid = blockIdx.x - gX, gA = gridDim.x - gX;
+    const double ia = st->inv_alpha, alpha = st->alpha, ib = st->inv_beta;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double su = 0.0;
+    for (int64_t s = (int64_t)bid * 4 + wid; s < nslices; s += (int64_t)gA * 4) {
+        const int64_t base = sp[s];
+        const double ax = sell_row_dot(ci, val, base, (sp[s + 1] - base) / SELL_C, lane, vt);
+        const int64_t row = s * SELL_C + lane;
+        if (row < m) {
+            const double un = ax * ia - alpha * (u[row] * ib);
+            u[row] = un;
+            su += un * un;
+        }
+    }
+    store_partial(su, part_u, bid);
+}
+
+// ---- SpMTV: ṽ' = (Aᵀ ũ)/β − β ṽ/α ; Σṽ'² --------------------------------------------------
+__global__ __launch_bounds__(BLOCK) void k_spmtv(const LsqState* __restrict__ st, int64_t n, int64_t nslices,
+                                                 const int64_t* __restrict__ sp, const int32_t* __restrict__ ci,
+                                                 const double* __restrict__ val, const double* __restrict__ u,
+                                                 const double* __restrict__ vin, double* __restrict__ vout,
+                                                 double* part_v) {
+    if (st->stop) return;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const double ib = st->inv_beta, beta = st->beta, ia = st->inv_alpha;
+    const bool skip = st->skip_v;
+    double sv = 0.0;
+    for (int64_t s = (int64_t)blockIdx.x * 4 + wid; s < nslices; s += (int64_t)gridDim.x * 4) {
+        const int64_t row = s * SELL_C + lane;
+        double vn;
+        if (skip) {
+            vn = row < n ? vin[row] : 0.0;
+        } else {
+            const int64_t base = sp[s];
+            const double atu = sell_row_dot(ci, val, base, (sp[s + 1] - base) / SELL_C, lane, u);
+            vn = row < n ? atu * ib - beta * (vin[row] * ia) : 0.0;
+        }
+        if (row < n) {
+            vout[row] = vn;
+            sv += vn * vn;
+        }
+    }
+    store_partial(sv, part_v, blockIdx.x);
+}
+
+// deterministic single-block sum of nparts partials
+__device__ double reduce_parts(const double* part, int nparts) {
+    __shared__ double red[4];
+    double a = 0.0;
+    for (int i = threadIdx.x; i < nparts; i += BLOCK) a += part[i];
+    return block_sum(a, red);  // valid in thread 0
+}
+
+// ---- β: 1-block kernel --------------------------------------------------------------------------
+// mode 0: iteration; mode 1: init (also bnorm from part_b)
+__global__ __launch_bounds__(BLOCK) void k_beta(LsqState* st, const double* part_u, int nu,
+                                                const double* part_b, int nb, int mode) {
+    if (mode == 0 && st->stop) {
+        if (threadIdx.x == 0) st->finished = 1;   // the final x/w update has been applied
+        return;
+    }
+    const double su = reduce_parts(part_u, nu);
+    double sb = 0.0;
+    if (mode == 1) sb = reduce_parts(part_b, nb);
+    if (threadIdx.x) return;
+    const double beta = sqrt(su);
+    st->beta = beta;
+    st->skip_v = !(beta > 0.0);
+    if (beta > 0.0) st->inv_beta = 1.0 / beta;
+    if (mode == 1) {
+        st->bnorm = sqrt(sb);
+        st->alpha = 0.0;
+        st->inv_alpha = 0.0;
+    } else if (beta > 0.0) {
+        const double a = st->alpha;
+        st->anorm = sqrt(st->anorm * st->anorm + a * a + beta * beta);
+    }
+}
+
+__device__ __forceinline__ double sgn(double x) { return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : 0.0); }
+
+// scipy _sym_ortho: stable Givens (c, s, r) with r = sqrt(a²+b²)
+__device__ void sym_ortho(double a, double b, double& c, double& s, double& r) {
+    if (b == 0.0) { c = sgn(a); s = 0.0; r = fabs(a); return; }
+    if (a == 0.0) { c = 0.0; s = sgn(b); r = fabs(b); return; }
+    if (fabs(b) > fabs(a)) {
+        const double tau = a / b;
+        s = sgn(b) / sqrt(1.0 + tau * tau);
+        c = s * tau;
+        r = b / s;
+    } else {
+        const double tau = b / a;
+        c = sgn(a) / sqrt(1.0 + tau * tau);
+        s = c * tau;
+        r = a / c;
+    }
+}
+
+// ---- α, rotation, norm estimates, stopping rules: 1-block kernel ----------------------------
+// mode 1: init (rhobar = α, φ̄ = β ...); mode 0: iteration
+__global__ __launch_bounds__(BLOCK) void k_givens(LsqState* st, const double* part_v, int nv,
+                                                  const double* part_w, int nw, int mode) {
+    if (mode == 0 && st->stop) return;
+    const double sv = reduce_parts(part_v, nv);
+    const double sw = reduce_parts(part_w, nw);
+    if (threadIdx.x) return;
+    const double eps = 2.220446049250313e-16;
+    if (!st->skip_v) {
+        const double alpha = sqrt(sv);
+        st->alpha = alpha;
+        st->inv_alpha = alpha > 0.0 ? 1.0 / alpha : 0.0;
+    }
+    const double alpha = st->alpha, beta = st->beta;
+    if (mode == 1) {
+        st->rhobar = alpha;
+        st->phibar = beta;
+        st->rnorm = beta;
+        st->r1norm = beta;
+        st->r2norm = beta;
+        st->arnorm = alpha * beta;
+        st->itn = 0;
+        st->have_xw = 0;
+        st->finished = 0;
+        st->stop = 0;
+        st->istop = 0;
+        if (alpha * beta == 0.0) {   // exact solution x = x0
+            st->stop = 1;
+            st->finished = 1;
+        }
+        return;
+    }
+    // ddnorm uses w before this iteration's update: ‖w_k‖² = sw (from the previous x/w pass)
+    st->itn += 1;
+    double cs, sn, rho;
+    sym_ortho(st->rhobar, beta, cs, sn, rho);
+    const double theta = sn * alpha;
+    st->rhobar = -cs * alpha;
+    const double phi = cs * st->phibar;
+    st->phibar = sn * st->phibar;
+    const double tau = sn * phi;
+    st->t1 = phi / rho;
+    st->t2 = -theta / rho;
+    st->ddnorm += sw / (rho * rho);
+    const double delta = st->sn2 * rho;
+    const double gambar = -st->cs2 * rho;
+    const double rhs = phi - delta * st->z;
+    const double zbar = rhs / gambar;
+    st->xnorm = sqrt(st->xxnorm + zbar * zbar);
+    const double gamma = sqrt(gambar * gambar + theta * theta);
+    st->cs2 = gambar / gamma;
+    st->sn2 = theta / gamma;
+    st->z = rhs / gamma;
+    st->xxnorm += st->z * st->z;
+    st->acond = st->anorm * sqrt(st->ddnorm);
+    const double res1 = st->phibar * st->phibar;
+    const double rnorm = sqrt(res1 + st->res2);
+    st->rnorm = rnorm;
+    st->arnorm = alpha * fabs(tau);
+    st->r1norm = rnorm;
+    st->r2norm = rnorm;
+    st->have_xw = 1;
+    const double bnorm = st->bnorm, anorm = st->anorm, xnorm = st->xnorm;
+    const double test1 = rnorm / bnorm;
+    const double test2 = st->arnorm / (anorm * rnorm + eps);
+    const double test3 = 1.0 / (st->acond + eps);
+    const double t1 = test1 / (1.0 + anorm * xnorm / bnorm);
+    const double rtol = st->btol + st->atol * anorm * xnorm / bnorm;
+    int istop = 0;
+    if (st->itn >= st->maxit) istop = 7;
+    if (!st->no_stop) {
+        if (1.0 + test3 <= 1.0) istop = 6;
+        if (1.0 + test2 <= 1.0) istop = 5;
+        if (1.0 + t1 <= 1.0) istop = 4;
+        if (test3 <= st->ctol) istop = 3;
+        if (test2 <= st->atol) istop = 2;
+        if (test1 <= rtol) istop = 1;
+    }
+    st->istop = istop;
+    if (istop) st->stop = 1;
+}
+
+// w = ṽ/α, y = y0 (or 0), Σw²
+__global__ __launch_bounds__(BLOCK) void k_init_w(const LsqState* __restrict__ st, int64_t n,
+                                                  const double* __restrict__ vt, const double* __restrict__ y0s,
+                                                  double* __restrict__ w, double* __restrict__ y, double* part_w) {
+    const double ia = st->inv_alpha;
+    double sw = 0.0;
+    for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLOCK) {
+        const double wj = vt[j] * ia;
+        w[j] = wj;
+        y[j] = y0s ? y0s[j] : 0.0;
+        sw += wj * wj;
+    }
+    store_partial(sw, part_w, blockIdx.x);
+}
+
+// y0s = x0 / cs  (warm start into preconditioned coordinates);  x = cs ∘ y on the way out
+__global__ __launch_bounds__(BLOCK) void k_scale(int64_t n, const double* __restrict__ a, const double* __restrict__ cs,
+                                                 int divide, double* __restrict__ out) {
+    for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLOCK)
+        out[j] = divide ? a[j] / cs[j] : a[j] * cs[j];
+}
+
+struct Grids {
+    int gA, gT, gX;
+};
+
+Grids grids_for(const System& S) {
+    Grids g;
+    g.gA = (int)std::min<int64_t>(std::max<int64_t>((S.A.nslices + 3) / 4, 1), NPART);
+    g.gT = (int)std::min<int64_t>(std::max<int64_t>((S.AT.nslices + 3) / 4, 1), NPART);
+    g.gX = grid_for(S.G.n, BLOCK * 4, NPART);
+    return g;
+}
+
+void ensure_workspace(System& S) {
+    const int64_t m = S.G.m, n = std::max<int64_t>(S.G.n, 1);
+    if (S.u.n != m) S.u.alloc(std::max<int64_t>(m, 1));
+    if (S.bw.n != m) S.bw.alloc(std::max<int64_t>(m, 1));
+    if (S.vb0.n != n) {
+        S.vb0.alloc(n);
+        S.vb1.alloc(n);
+        S.w.alloc(n);
+        S.y.alloc(n);
+    }
+    if (!S.part_u.p) {
+        S.part_u.alloc(NPART);
+        S.part_v.alloc(NPART);
+        S.part_w.alloc(NPART);
+        S.part_b.alloc(NPART);
+        S.st.alloc(1);
+    }
+}
+
+// launch one LSQR iteration; parity p: ṽ read from vb[p], written to vb[1-p]
+void launch_iteration(System& S, const Grids& g, int p) {
+    hipStream_t st = S.stream;
+    double* vt = p ? S.vb1.p : S.vb0.p;
+    double* vo = p ? S.vb0.p : S.vb1.p;
+    hipLaunchKernelGGL(k_xw_spmv, dim3(g.gX + g.gA), dim3(BLOCK), 0, st, S.st.p, g.gX, S.G.n, S.y.p, S.w.p, vt, S.G.m,
+                       S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p, S.u.p, S.part_u.p, S.part_w.p);
+    hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gA, S.part_b.p, 0, 0);
+    hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, S.G.n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
+                       S.AT.val.p, S.u.p, vt, vo, S.part_v.p);
+    hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gT, S.part_w.p, g.gX, 0);
+}
+
+}  // namespace
+
+// Initialise the LSQR state from rhs b (host, length m, unweighted) and optional warm start
+// x0 (host, length n, or nullptr).  Mirrors scipy lsqr's set-up block.
+void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts& o, bool no_stop) {
+    hipStream_t st = S.stream;
+    ensure_workspace(S);
+    const Grids g = grids_for(S);
+    const int64_t m = S.G.m, n = S.G.n;
+    DBuf<double> db(std::max<int64_t>(m, 1));
+    db.upload(h_b, m, st);
+    DBuf<double> dy0;
+    if (h_x0) {
+        dy0.alloc(std::max<int64_t>(n, 1));
+        dy0.upload(h_x0, n, st);
+        hipLaunchKernelGGL(k_scale, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, dy0.p, S.cs.p, 1, dy0.p);
+        KERNEL_CHECK();
+    }
+    LsqState h{};
+    h.atol = o.atol;
+    h.btol = o.btol;
+    h.ctol = o.conlim > 0 ? 1.0 / o.conlim : 0.0;
+    h.maxit = o.maxit > 0 ? o.maxit : 4 * std::max<int64_t>(n, 1);
+    h.no_stop = no_stop ? 1 : 0;
+    h.cs2 = -1.0;
+    HIP_CHECK(hipMemcpyAsync(S.st.p, &h, sizeof(h), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_init_u, dim3(g.gA), dim3(BLOCK), 0, st, m, S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p,
+                       S.rs.p, db.p, dy0.p, S.u.p, S.bw.p, S.part_u.p, S.part_b.p);
+    KERNEL_CHECK();
+    hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gA, S.part_b.p, g.gA, 1);
+    KERNEL_CHECK();
+    S.vb1.zero(st);
+    hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
+                       S.AT.val.p, S.u.p, S.vb1.p, S.vb0.p, S.part_v.p);
+    KERNEL_CHECK();
+    hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gT, S.part_w.p, g.gX, 1);
+    KERNEL_CHECK();
+    hipLaunchKernelGGL(k_init_w, dim3(g.gX), dim3(BLOCK), 0, st, S.st.p, n, S.vb0.p, dy0.p, S.w.p, S.y.p,
+                       S.part_w.p);
+    KERNEL_CHECK();
+    HIP_CHECK(hipStreamSynchronize(st));   // db / dy0 are released on return
+    S.iter_parity = 0;
+}
+
+namespace {
+
+struct GraphCache {
+    const System* sys = nullptr;
+    const void* key = nullptr;   // S.u.p identifies the workspace generation
+    int batch = 0;
+    hipGraphExec_t exec = nullptr;
+};
+thread_local GraphCache g_cache;
+
+// run `count` iterations starting at parity S.iter_parity (count even when graphs are used)
+void run_batch(System& S, int count, bool use_graph) {
+    const Grids g = grids_for(S);
+    if (use_graph && count % 2 == 0 && S.iter_parity == 0) {
+        GraphCache& c = g_cache;
+        if (c.exec == nullptr || c.sys != &S || c.key != (const void*)S.u.p || c.batch != count) {
+            if (c.exec) (void)hipGraphExecDestroy(c.exec);
+            c.exec = nullptr;
+            hipGraph_t graph;
+            HIP_CHECK(hipStreamBeginCapture(S.stream, hipStreamCaptureModeThreadLocal));
+            for (int i = 0; i < count; ++i) launch_iteration(S, g, i & 1);
+            HIP_CHECK(hipStreamEndCapture(S.stream, &graph));
+            HIP_CHECK(hipGraphInstantiate(&c.exec, graph, nullptr, nullptr, 0));
+            HIP_CHECK(hipGraphDestroy(graph));
+            c.sys = &S;
+            c.key = S.u.p;
+            c.batch = count;
+        }
+        HIP_CHECK(hipGraphLaunch(c.exec, S.stream));
+        return;
+    }
+    for (int i = 0; i < count; ++i) {
+        launch_iteration(S, g, S.iter_parity);
+        S.iter_parity ^= 1;
+    }
+    KERNEL_CHECK();
+}
+
+double bytes_per_iter(const System& S) {
+    const double Z = (double)S.G.nnz, m = (double)S.G.m, n = (double)S.G.n;
+    return 24.0 * Z + 24.0 * m + 64.0 * n;   // DESIGN.md §Byte model
+}
+
+void fill_stats(const LsqState& h, lsq_stats* s) {
+    s->iters = h.itn;
+    s->istop = h.istop;
+    s->r1norm = h.r1norm;
+    s->r2norm = h.r2norm;
+    s->anorm = h.anorm;
+    s->acond = h.acond;
+    s->arnorm = h.arnorm;
+    s->xnorm = h.xnorm;
+}
+
+}  // namespace
+
+void graph_cache_drop(const System* S) {
+    if (g_cache.sys == S && g_cache.exec) {
+        (void)hipGraphExecDestroy(g_cache.exec);
+        g_cache = GraphCache{};
+    }
+}
+
+int lsqr_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq_stats* stats) {
+    refresh_scaling(S, o.precond);
+    lsqr_init(S, h_b, o.use_x0 ? h_x : nullptr, o, false);
+    int batch = o.batch > 0 ? o.batch : 16;
+    batch += batch & 1;
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    HIP_CHECK(hipEventRecord(e0, S.stream));
+    LsqState h{};
+    HIP_CHECK(hipMemcpyAsync(&h, S.st.p, sizeof(h), hipMemcpyDeviceToHost, S.stream));
+    HIP_CHECK(hipStreamSynchronize(S.stream));
+    while (!h.stop) {
+        run_batch(S, batch, o.use_graph != 0);
+        HIP_CHECK(hipMemcpyAsync(&h, S.st.p, sizeof(h), hipMemcpyDeviceToHost, S.stream));
+        HIP_CHECK(hipStreamSynchronize(S.stream));
+    }
+    if (!h.finished) {   // apply the final x/w update
+        S.iter_parity = 0;
+        const Grids g = grids_for(S);
+        // after an even batch the newest ṽ is in vb0; the flush only needs the x/w part
+        hipLaunchKernelGGL(k_xw_spmv, dim3(g.gX + g.gA), dim3(BLOCK), 0, S.stream, S.st.p, g.gX, S.G.n, S.y.p, S.w.p,
+                           S.vb0.p, S.G.m, S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p, S.u.p, S.part_u.p,
+                           S.part_w.p);
+        hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, S.stream, S.st.p, S.part_u.p, g.gA, S.part_b.p, 0, 0);
+        KERNEL_CHECK();
+    }
+    HIP_CHECK(hipEventRecord(e1, S.stream));
+    const int64_t n = S.G.n;
+    hipLaunchKernelGGL(k_scale, dim3(grid_for(n)), dim3(BLOCK), 0, S.stream, n, S.y.p, S.cs.p, 0, S.vb1.p);
+    KERNEL_CHECK();
+    S.vb1.download(h_x, n, S.stream);
+    HIP_CHECK(hipMemcpyAsync(&h, S.st.p, sizeof(h), hipMemcpyDeviceToHost, S.stream));
+    HIP_CHECK(hipStreamSynchronize(S.stream));
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (stats) {
+        fill_stats(h, stats);
+        stats->time_s = ms * 1e-3;
+        stats->bytes_per_iter = bytes_per_iter(S);
+    }
+    S.iter_ready = false;   // the solve consumed the iteration state
+    return h.istop == 7 ? 1 : 0;
+}
+
+int lsqr_iterate(System& S, const double* h_b, int64_t iters, const lsq_opts& o, lsq_stats* stats) {
+    refresh_scaling(S, o.precond);
+    if (!S.iter_ready) {
+        lsq_opts oo = o;
+        oo.maxit = INT64_MAX / 4;
+        lsqr_init(S, h_b, nullptr, oo, true);
+        S.iter_ready = true;
+    }
+    int batch = o.batch > 0 ? o.batch : 16;
+    batch += batch & 1;
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    HIP_CHECK(hipEventRecord(e0, S.stream));
+    int64_t left = iters;
+    while (left > 0) {
+        const int c = (int)std::min<int64_t>(left, batch);
+        run_batch(S, c, o.use_graph != 0 && c == batch);
+        left -= c;
+    }
+    HIP_CHECK(hipEventRecord(e1, S.stream));
+    LsqState h{};
+    HIP_CHECK(hipMemcpyAsync(&h, S.st.p, sizeof(h), hipMemcpyDeviceToHost, S.stream));
+    HIP_CHECK(hipStreamSynchronize(S.stream));
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (stats) {
+        fill_stats(h, stats);
+        stats->time_s = ms * 1e-3;
+        stats->bytes_per_iter = bytes_per_iter(S);
+    }
+    return 0;
+}
+
+// Time each iteration kernel in isolation (reps launches, HIP events on the handle's stream).
+// Destroys the iteration state; used by bench.py for the per-kernel roofline.
+void lsqr_profile(System& S, int reps, double* ms_out /* [4]: xw_spmv, spmtv, beta, givens */) {
+    ensure_workspace(S);
+    const Grids g = grids_for(S);
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    LsqState h{};
+    h.alpha = 1.0; h.inv_alpha = 1.0; h.beta = 1.0; h.inv_beta = 1.0; h.have_xw = 1; h.t1 = 1e-3; h.t2 = -1e-3;
+    h.maxit = INT64_MAX / 4; h.no_stop = 1; h.bnorm = 1.0; h.cs2 = -1.0;
+    HIP_CHECK(hipMemcpyAsync(S.st.p, &h, sizeof(h), hipMemcpyHostToDevice, S.stream));
+    for (int k = 0; k < 4; ++k) {
+        for (int pass = 0; pass < 2; ++pass) {   // pass 0 = warm-up
+            HIP_CHECK(hipEventRecord(e0, S.stream));
+            for (int r = 0; r < reps; ++r) {
+                if (k == 0)
+                    hipLaunchKernelGGL(k_xw_spmv, dim3(g.gX + g.gA), dim3(BLOCK), 0, S.stream, S.st.p, g.gX, S.G.n,
+                                       S.y.p, S.w.p, S.vb0.p, S.G.m, S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p,
+                                       S.u.p, S.part_u.p, S.part_w.p);
+                else if (k == 1)
+                    hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, S.stream, S.st.p, S.G.n, S.AT.nslices,
+                                       S.AT.sp.p, S.AT.ci.p, S.AT.val.p, S.u.p, S.vb0.p, S.vb1.p, S.part_v.p);
+                else if (k == 2)
+                    hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, S.stream, S.st.p, S.part_u.p, g.gA,
+                                       S.part_b.p, 0, 2);
+                else
+                    hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, S.stream, S.st.p, S.part_v.p, g.gT,
+                                       S.part_w.p, g.gX, 2);
+            }
+            HIP_CHECK(hipEventRecord(e1, S.stream));
+            HIP_CHECK(hipEventSynchronize(e1));
+        }
+        float ms = 0.f;
+        HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        ms_out[k] = ms / reps;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    S.iter_ready = false;
+}
+
+}  // namespace lsq

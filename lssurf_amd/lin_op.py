@@ -1,0 +1,433 @@
+"""Sparse linear operators on fd_grid nodes (COO triplets + table of contents).
+
+Host mirror of LSsurf/lin_op.py:12-753.  Every method that the solve path uses reproduces the
+reference's triplets (r, c, v), ``ind0`` and TOC exactly, in the same order and with
+bit-identical coefficients:
+
+  diff_op        lin_op.py:80-132   constant-coefficient template at every centre whose
+                                    template fits in the grid (meshgrid 'ij' order)
+  one/grad/grad2/grad_dzdt/grad2_dzdt/d2z_dt2/dzdt/diff   lin_op.py:249-309 (stencil table below)
+  interp_mtx     lin_op.py:163-247  bi/trilinear weights into the 2^N surrounding nodes
+  add / vstack   lin_op.py:134-161, 555-631
+  toCSR          lin_op.py:745-753  (drop exact zeros, sum duplicates)
+  mask_for_ind0, normalize_by_unit_product, grid_prod, grid_error, update_dst_grid
+
+In addition each operator records its *structure* (``parts``): which stencil or interpolation
+generated which rows.  lssurf_amd's device path uses it to know an operator is a pure
+stencil/interp operator; methods that rescale values by data (normalize_by_unit_product,
+masks) drop the structure.
+"""
+import numpy as np
+import scipy.sparse as sp
+
+from .fd_grid import fd_grid
+
+# Stencil table: (name suffix, per-dimension offsets, coefficient numerator array, denominator
+# expression) — the denominators are evaluated with the reference's exact operation order.
+
+
+def _grad_parts(g, DOF):
+    c = np.array([-1., 1.]) / (g.delta[0])
+    return [('d' + DOF + '_dx', ([0, 0], [-1, 0]), c),
+            ('d' + DOF + '_dy', ([-1, 0], [0, 0]), c)]
+
+
+def _grad2_parts(g, DOF):
+    c = np.array([-1., 2., -1.]) / (g.delta[0] ** 2)
+    cxy = 0.5 * np.array([-1., 1., 1., -1]) / (g.delta[0] ** 2)
+    return [('d2' + DOF + '_dx2', ([0, 0, 0], [-1, 0, 1]), c),
+            ('d2' + DOF + '_dy2', ([-1, 0, 1], [0, 0, 0]), c),
+            ('d2' + DOF + '_dxdy', ([-1, -1, 1, 1], [-1, 1, -1, 1]), cxy)]
+
+
+def _grad_dzdt_parts(g, DOF, t):
+    c = np.array([-1., 1., 1., -1.]) / (t * g.delta[0] * g.delta[2])
+    return [('d2' + DOF + '_dxdt', ([0, 0, 0, 0], [-1, 0, -1, 0], [-t, -t, 0, 0]), c),
+            ('d2' + DOF + '_dydt', ([-1, 0, -1, 0], [0, 0, 0, 0], [-t, -t, 0, 0]), c)]
+
+
+def _grad2_dzdt_parts(g, DOF, t):
+    c = np.array([-1., 2., -1., 1., -2., 1.]) / (t * g.delta[0] ** 2. * g.delta[2])
+    cxy = np.array([-1., 1., 1., -1., 1., -1., -1., 1.]) / (g.delta[0] ** 2 * g.delta[2])
+    return [('d3' + DOF + '_dx2dt', ([0, 0, 0, 0, 0, 0], [-1, 0, 1, -1, 0, 1], [-t, -t, -t, 0, 0, 0]), c),
+            ('d3' + DOF + '_dy2dt', ([-1, 0, 1, -1, 0, 1], [0, 0, 0, 0, 0, 0], [-t, -t, -t, 0, 0, 0]), c),
+            ('d3' + DOF + '_dxdydt', ([-1, 0, -1, 0, -1, 0, -1, 0], [-1, -1, 0, 0, -1, -1, 0, 0],
+                                      [-t, -t, -t, -t, 0, 0, 0, 0]), cxy)]
+
+
+class lin_op:
+    def __init__(self, grid=None, row_0=0, col_N=None, col_0=None, name=None):
+        self.grid = grid
+        self.col_0 = col_0 if col_0 is not None else (grid.col_0 if grid is not None else None)
+        self.col_N = col_N if col_N is not None else (grid.col_N if grid is not None else None)
+        self.row_0 = row_0
+        self.N_eq = 0
+        self.name = name
+        self.id = None
+        self.r = np.array([], dtype=int)
+        self.c = np.array([], dtype=int)
+        self.v = np.array([], dtype=float)
+        self.ind0 = np.zeros([0], dtype=int)
+        self.TOC = {'rows': {}, 'cols': {}}
+        self.dst_grid = None
+        self.dst_ind0 = None
+        self.expected = None
+        self.prior = None
+        self.shape = None
+        self.size = None
+        self.parts = []   # structure records (see module docstring)
+
+    def __update_size_and_shape__(self):
+        self.shape = (self.N_eq, self.col_N)
+
+    # ---- helpers ---------------------------------------------------------------------------
+    def apply_xform(self, pts, xform=None, dims=(0, 1)):
+        if xform is None:
+            xform = self.grid.xform
+        if xform is None:
+            return pts
+        P = np.c_[[np.ravel(p) for p in pts[0:len(xform['origin'])]]].T
+        T = (P - xform['origin']) @ xform['basis_vectors']
+        return [T[:, d].ravel() for d in dims]
+
+    def ravel(self):
+        self.r, self.c, self.v = np.ravel(self.r), np.ravel(self.c), np.ravel(self.v)
+        return self
+
+    def fix_dtypes(self):
+        self.r = self.r.astype(int)
+        self.c = self.c.astype(int)
+
+    # ---- stencils ----------------------------------------------------------------------------
+    def diff_op(self, delta_subs, vals, which_nodes=None, valid_equations_only=True):
+        g = self.grid
+        nd = min(len(delta_subs), g.N_dims)   # extra offset rows are ignored (zip semantics)
+        lo = [max(0, -int(np.min(ds))) if valid_equations_only else 0 for ds in delta_subs]
+        hi = [min(int(g.shape[k]), int(g.shape[k]) - int(np.max(delta_subs[k])))
+              if valid_equations_only else int(g.shape[k]) for k in range(nd)]
+        centres = [s.ravel() for s in np.meshgrid(*[np.arange(a, b) for a, b in zip(lo, hi)], indexing='ij')]
+        if which_nodes is not None:
+            keep = np.isin(g.global_ind(centres), which_nodes)
+            centres = [s[keep] for s in centres]
+        n_eq, n_tpl = centres[0].size, len(delta_subs[0])
+        R = np.empty((n_eq, n_tpl), dtype=int)
+        C = np.empty((n_eq, n_tpl), dtype=int)
+        V = np.empty((n_eq, n_tpl), dtype=float)
+        rows = self.row_0 + np.arange(0, n_eq, dtype=int)
+        for k in range(n_tpl):
+            sub = [centres[d] + delta_subs[d][k] for d in range(nd)]
+            R[:, k] = rows
+            if valid_equations_only:
+                C[:, k] = g.global_ind(sub)
+                V[:, k] = np.ravel(vals[k])
+            else:
+                C[:, k], ok = g.global_ind(sub, return_valid=True)
+                V[:, k] = np.ravel(vals[k]) * np.ravel(ok)
+        self.r, self.c, self.v = R, C, V
+        self.N_eq = n_eq
+        self.ind0 = g.global_ind(centres).ravel()
+        self.TOC['rows'] = {self.name: range(self.N_eq)}
+        self.TOC['cols'] = {g.name: np.arange(g.col_0, g.col_0 + g.N_nodes)}
+        simple = valid_equations_only and which_nodes is None
+        self.parts = [dict(kind='stencil', grid=g, subs=[list(map(int, ds)) for ds in delta_subs[:nd]],
+                           vals=np.array([float(np.ravel(vals[k])[0]) for k in range(n_tpl)]),
+                           row0=0, n_eq=n_eq)] if simple and all(np.size(vv) == 1 for vv in vals) else None
+        self.__update_size_and_shape__()
+        return self
+
+    def _stack_named(self, parts):
+        subops = [lin_op(self.grid, name=nm).diff_op(subs, coeffs) for nm, subs, coeffs in parts]
+        return self.vstack(tuple(subops))
+
+    def one(self, DOF='z', which_nodes=None):
+        self.diff_op([[0]] * len(self.grid.shape), np.array([1.]), which_nodes=which_nodes)
+        self.__update_size_and_shape__()
+        return self
+
+    def grad(self, DOF='z'):
+        self._stack_named(_grad_parts(self.grid, DOF))
+        self.__update_size_and_shape__()
+        return self
+
+    def grad2(self, DOF='z'):
+        self._stack_named(_grad2_parts(self.grid, DOF))
+        self.__update_size_and_shape__()
+        return self
+
+    def grad_dzdt(self, DOF='z', t_lag=1):
+        self._stack_named(_grad_dzdt_parts(self.grid, DOF, t_lag))
+        self.__update_size_and_shape__()
+        return self
+
+    def grad2_dzdt(self, DOF='z', t_lag=1):
+        self._stack_named(_grad2_dzdt_parts(self.grid, DOF, t_lag))
+        self.__update_size_and_shape__()
+        return self
+
+    def diff(self, lag=1, dim=0):
+        offs = [[0, 0] for _ in range(self.grid.N_dims)]
+        offs[dim] = [0, lag]
+        self.diff_op(offs, np.array([-1., 1.]) / (lag * self.grid.delta[dim]))
+        self.__update_size_and_shape__()
+        return self
+
+    def dzdt(self, lag=1, DOF='dz'):
+        self.diff_op(([0, 0], [0, 0], [0, lag]), np.array([-1., 1.]) / (lag * self.grid.delta[2]))
+        self.__update_size_and_shape__()
+        self.update_dst_grid([0, 0, 0.5 * lag * self.grid.delta[2]], np.array([1, 1, 1]))
+        return self
+
+    def d2z_dt2(self, DOF='dz', t_lag=1):
+        # the reference returns a NEW operator named 'd2'+DOF+'_dt2' (lin_op.py:286-290)
+        op = lin_op(self.grid, name='d2' + DOF + '_dt2').diff_op(
+            ([0, 0, 0], [0, 0, 0], [-t_lag, 0, t_lag]), np.array([-1, 2, -1]) / ((t_lag * self.grid.delta[2]) ** 2))
+        op.__update_size_and_shape__()
+        return op
+
+    # ---- interpolation -----------------------------------------------------------------------
+    def interp_mtx(self, pts_in, xform=None, dims=None, bounds_error=True):
+        g = self.grid
+        if xform is None and g.xform is not None:
+            xform = g.xform
+        if dims is None:
+            dims = np.arange(g.N_dims, dtype=int)
+        pts = self.apply_xform(pts_in, xform, dims) if xform is not None else [np.ravel(p) for p in pts_in]
+        rows = np.flatnonzero(g.validate_pts(pts))
+        if bounds_error and rows.size < len(pts[0]):
+            raise ValueError(f'Found {len(pts[0]) - rows.size} points out of bounds for grid {g.name}')
+        pts = [p[rows] for p in pts]
+        fsub = g.float_sub(pts)
+        cell = g.cell_sub_for_pts(pts)
+        frac = [a - b for a, b in zip(fsub, cell)]
+        base = g.global_ind(cell)
+        corners = np.c_[[k.ravel() for k in np.mgrid[tuple(slice(0, 2) for _ in range(g.N_dims))]]] \
+            if g.N_dims > 1 else np.array([[0, 1]])
+        n_nb, npts = corners.shape[1], rows.size
+        R = np.zeros([npts, n_nb], dtype=int)
+        C = np.zeros([npts, n_nb], dtype=int)
+        V = np.ones([npts, n_nb], dtype=float)
+        for k in range(n_nb):
+            R[:, k] = rows
+            C[:, k] = base + np.sum(g.stride * corners[:, k])
+            for d in range(g.N_dims):
+                V[:, k] *= frac[d] if corners[d, k] else (1. - frac[d])
+        self.r, self.c, self.v = R, C, V
+        self.N_eq = npts
+        self.ind0 = np.arange(0, npts, dtype='int')
+        self.TOC['rows'] = {self.name: np.arange(self.N_eq, dtype='int')}
+        self.TOC['cols'] = {g.name: np.arange(g.col_0, g.col_0 + g.N_nodes)}
+        self.parts = [dict(kind='interp', grid=g, pts=pts, rows=rows, row0=0, n_eq=npts)] \
+            if xform is None and bounds_error else None
+        self.__update_size_and_shape__()
+        return self
+
+    # ---- composition -------------------------------------------------------------------------
+    def add(self, op):
+        if isinstance(op, (list, tuple)):
+            for each in op:
+                self.add(each)
+            return self
+        self.r = np.append(self.r, op.r)
+        self.c = np.append(self.c, op.c)
+        self.v = np.append(self.v, op.v)
+        self.ind0 = np.append(self.ind0, op.ind0)
+        for key, cols in op.TOC['cols'].items():
+            self.TOC['cols'][key] = cols
+        self.col_N = np.maximum(self.col_N, op.col_N)
+        if self.parts is not None and op.parts is not None:
+            self.parts = self.parts + op.parts       # same rows, summed operators
+        else:
+            self.parts = None
+        self.__update_size_and_shape__()
+        return self
+
+    def vstack(self, ops, order=None, name=None, TOC_cols=None):
+        if isinstance(ops, lin_op):
+            ops = (self, ops)
+        order = range(len(ops)) if order is None else order
+        if name is not None:
+            self.name = name
+        if TOC_cols is None:
+            TOC_cols = {}
+            every = []
+            for op in ops:
+                for key, cols in op.TOC['cols'].items():
+                    TOC_cols[key] = cols
+                    every.append(np.asarray(cols))
+            if self.name is not None:
+                TOC_cols[self.name] = np.unique(np.concatenate(every)) if every else np.array([], int)
+        if self.col_N is None:
+            self.col_N = np.max(np.array([op.col_N for op in ops]))
+        self.TOC['cols'] = TOC_cols
+        rr, cc, vv, ee, parts = [], [], [], [], []
+        offset = 0
+        for i in order:
+            op = ops[i]
+            rr.append(np.ravel(op.r) + offset)
+            cc.append(np.ravel(op.c))
+            vv.append(np.ravel(op.v))
+            if op.expected is not None:
+                ee.append(np.ravel(op.expected))
+            label = op.name if op.name is not None else 'eq'
+            base, k = label, 0
+            while label in self.TOC['rows']:
+                k += 1
+                label = f'{base}_{k}'
+            pieces = []
+            for key, rows in op.TOC['rows'].items():
+                shifted = np.array(rows, dtype='int') + offset
+                self.TOC['rows'][key] = shifted
+                pieces.append(shifted.ravel())
+            if label not in self.TOC['rows']:
+                self.TOC['rows'][label] = np.concatenate(pieces)
+            if parts is not None and op.parts is not None:
+                parts.extend(dict(p, row0=p['row0'] + offset) for p in op.parts)
+            else:
+                parts = None
+            offset += op.N_eq
+        self.N_eq = offset
+        self.r, self.c, self.v = np.concatenate(rr), np.concatenate(cc), np.concatenate(vv)
+        if ee:
+            self.expected = np.concatenate(ee)
+        self.ind0 = np.concatenate([op.ind0 for op in ops])
+        if self.name is not None and len(self.name) > 0:
+            self.TOC['rows'][self.name] = np.arange(0, offset)
+        self.parts = parts
+        self.__update_size_and_shape__()
+        return self
+
+    # ---- masks, normalisation ----------------------------------------------------------------
+    def mask_for_ind0(self, mask_scale=None, mask=None):
+        if mask is None:
+            mask = self.grid.mask
+        if mask is None:
+            return np.ones_like(self.ind0, dtype=float)
+        rel = self.ind0 - self.grid.col_0
+        if len(self.grid.shape) > len(mask.shape):
+            subs = tuple(np.unravel_index(rel, self.grid.shape)[:len(mask.shape)])
+        else:
+            subs = np.unravel_index(rel, mask.shape)
+        sampled = mask[subs]
+        if mask_scale is None:
+            return sampled
+        out = np.zeros_like(sampled, dtype=float)
+        for key, val in mask_scale.items():
+            out[sampled == key] = val
+        return out
+
+    def normalize_by_unit_product(self, wt=1):
+        absop = lin_op(col_N=self.col_N)
+        absop.N_eq = self.N_eq
+        absop.r, absop.c, absop.v = self.r, self.c, np.abs(self.v)
+        absop.__update_size_and_shape__()
+        norm = absop.toCSR(row_N=absop.N_eq).dot(np.ones(self.shape[1]))
+        scale = np.zeros_like(norm)
+        scale[norm > 0] = 1. / norm[norm > 0]
+        self.v *= scale[self.r] * wt
+        self.parts = None
+
+    def sum_to_grid3(self, kernel_size, sub0s=None, lag=None, taper=True, valid_equations_only=True, dims=None):
+        """Sum (tapered) blocks of nodes onto a coarser output grid (lin_op.py:404-488)."""
+        g = self.grid
+        kernel_size = np.asarray(kernel_size)
+        half = np.floor((kernel_size - 1) / 2).astype(int) if taper else np.floor(kernel_size / 2).astype(int)
+        dims = list(range(len(g.shape))) if dims is None else list(dims)
+        nd = len(dims)
+        if sub0s is None:
+            if taper and valid_equations_only:
+                axes = [np.arange(half[i] + 1, g.shape[i], kernel_size[i] - 1, dtype=int) for i in dims]
+            elif taper:
+                axes = [np.arange(0, g.shape[i] + 1, kernel_size[i] - 1, dtype=int) for i in dims]
+            else:
+                axes = [np.arange(half[i], g.shape[i], kernel_size[i], dtype=int) for i in dims]
+            sub0s = np.meshgrid(*axes, indexing='ij')
+        ind0 = g.global_ind(sub0s[0:nd])
+        if np.mod(kernel_size[0] / 2, 1) == 0:
+            di, dj = np.meshgrid(np.arange(-half[0], half[0]), np.arange(-half[1], half[1]), indexing='ij')
+            grid_shift = [-g.delta[0] / 2, -g.delta[1] / 2, 0][0:nd]
+        else:
+            di, dj = np.meshgrid(np.arange(-half[0], half[0] + 1), np.arange(-half[1], half[1] + 1), indexing='ij')
+            grid_shift = [0, 0, 0][0:nd]
+        w0 = np.ones(kernel_size[0:2], dtype=float)
+        if taper:
+            for edge in (0, -1):
+                w0[edge, :] /= 2
+                w0[:, edge] /= 2
+        w0 = w0.ravel()
+        di, dj = di.ravel(), dj.ravel()
+        if lag is None:
+            offsets = [di, dj, np.zeros_like(di)]
+            wt = w0
+            grid_shift = [0, 0, 0]
+        else:
+            offsets = [np.concatenate([di, di]), np.concatenate([dj, dj]),
+                       np.concatenate([np.zeros_like(di, dtype=int), np.zeros_like(di, dtype=int) + lag])]
+            wt = np.concatenate([-w0, w0]) / (lag * g.delta[2])
+            grid_shift[2] = 0.5 * lag * g.delta[2]
+        self.diff_op(offsets, wt.astype(float), which_nodes=ind0, valid_equations_only=valid_equations_only)
+        self.update_dst_grid(grid_shift, np.maximum(1, kernel_size - 1) if taper else kernel_size)
+        return self
+
+    def update_dst_grid(self, grid_shift, kernel_size):
+        rcv0 = np.unravel_index(self.ind0 - self.grid.col_0, self.grid.shape)
+        dims = range(len(self.grid.shape))
+        bounds = [[self.grid.ctrs[d][rcv0[d][j]] + grid_shift[d] for j in (0, -1)] for d in dims]
+        self.dst_grid = fd_grid(bounds, kernel_size * self.grid.delta, name=self.name)
+        out_subs = [((rcv0[d] - rcv0[d][0]) / kernel_size[d]).astype(int) for d in dims]
+        self.dst_ind0 = np.ravel_multi_index(out_subs, self.dst_grid.shape)
+        return self
+
+    def data_bias(self, ind=None, val=None, col=None, DOF=None):
+        if col is None:
+            col = self.col_N
+            self.col_N += 1
+        self.r = ind
+        self.c = np.zeros_like(ind, dtype='int') + col
+        self.v = np.ones_like(ind, dtype='float') if val is None else val.ravel()
+        self.TOC['rows'] = {self.name: np.unique(self.r)}
+        self.TOC['cols'] = {self.name: np.unique(self.c)}
+        self.N_eq = np.max(ind) + 1
+        self.parts = None
+        self.__update_size_and_shape__()
+        return self
+
+    # ---- products on solutions ---------------------------------------------------------------
+    def _out_grid_and_rows(self, grid):
+        if grid is None:
+            grid = self.grid if self.dst_grid is None else self.dst_grid
+        rows = self.ind0 if self.dst_ind0 is None else self.dst_ind0
+        return grid, rows
+
+    def grid_prod(self, m, grid=None):
+        grid, rows = self._out_grid_and_rows(grid)
+        P = np.zeros(grid.col_N + 1) + np.nan
+        P[rows] = self.toCSR(row_N=rows.size, col_N=m.size).dot(m).ravel()
+        return P[grid.col_0:grid.col_N].reshape(grid.shape)
+
+    def grid_error(self, Rinv, grid=None):
+        grid, rows = self._out_grid_and_rows(grid)
+        E = np.zeros(self.col_N) + np.nan
+        E[rows] = np.sqrt((self.toCSR(row_N=rows.size, col_N=Rinv.shape[0]).dot(Rinv)).power(2).sum(axis=1)).ravel()
+        return E[grid.col_0:grid.col_N].reshape(grid.shape)
+
+    def print_TOC(self):
+        for rc in ('cols', 'rows'):
+            print(rc)
+            first = {k: np.min(self.TOC[rc][k]) for k in self.TOC[rc]}
+            for key in sorted(first, key=first.get):
+                print('\t%s\t%d : %d' % (key, np.min(self.TOC[rc][key]), np.max(self.TOC[rc][key])))
+
+    def toCSR(self, col_N=None, row_N=None):
+        if col_N is None:
+            col_N = self.col_N
+        self.fix_dtypes()
+        nz = np.ravel(self.v) != 0
+        r = np.ravel(self.r)[nz]
+        if row_N is None:
+            row_N = np.max(r) + 1
+        return sp.csr_matrix((np.ravel(self.v)[nz], (r, np.ravel(self.c)[nz])), shape=(row_N, col_N))
+
+    def triplets(self):
+        """(r, c, v) flattened, int64/int64/float64 — the COO handed to the device."""
+        return (np.ravel(self.r).astype(np.int64), np.ravel(self.c).astype(np.int64),
+                np.ravel(self.v).astype(np.float64))

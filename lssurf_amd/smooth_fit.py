@@ -1,0 +1,360 @@
+"""smooth_fit — the drop-in driver, with the least-squares solve on an MI355X.
+
+Call surface and return value follow LSsurf/smooth_fit.py:354-717 (``smooth_fit(**kwargs)``:
+required data, W, ctr, spacing, E_RMS; defaults of :356-401; returns m, E, data, grids,
+valid_data, TOC, R, RMS, timing, E_RMS, dzdt_lags; ``return_fit_objects`` early return of
+:639-645).  What changes is underneath:
+
+* system formation (smooth_fit.py:588-627) builds the same lin_ops on the host, but the
+  weighted, column-reduced matrix ``Ip_r·TCinv·[G_data; Gc]·Ip_c`` is formed ON THE DEVICE
+  once (``FitSystem``); outer iterations only re-weight and re-mask rows;
+* ``sparseqr.solve`` (:142) becomes device LSQR with a warm start from the previous outer
+  iteration; the residual ``G_data·m0`` (:146, :662) is a device SpMV;
+* everything else (editing, sigma_extra, convergence tests, parse_model) keeps the reference's
+  logic on the host.
+
+Options that add columns/rows outside the fd_grid model (biases, sensor grids, jitter,
+priors, lagrangian grids, averaging masks) are outside lssurf_amd's scope and raise
+NotImplementedError instead of silently changing the fit.
+"""
+from time import ctime, time
+
+import numpy as np
+
+from . import containers as pc
+from .calc_sigma_extra import RDE, calc_sigma_extra, calc_sigma_extra_on_grid
+from .constraint_functions import build_reference_epoch_matrix, reference_epoch_keep_cols, \
+    setup_smoothness_constraints
+from .grid_functions import setup_averaging_ops, setup_avg_mask_ops, setup_grids, setup_z0_avg, \
+    validate_by_dz_mask
+from .lin_op import lin_op
+from .solver import LSQSolver
+
+DEFAULTS = {'reference_epoch': 0, 'W_ctr': 1e4, 'return_fit_objects': False, 'mask_file': None,
+            'mask_data': None, 'mask_update_function': None, 'mask_scale': {0: 10, 1: 1}, 'compute_E': False,
+            'max_iterations': 10, 'min_iterations': 2, 'sigma_extra_relax': False,
+            'sigma_extra_bin_spacing': None, 'sigma_extra_max': None, 'sigma_extra_keys': None,
+            'srs_proj4': None, 'N_subset': None, 'bias_params': None, 'bias_filter': None, 'repeat_res': None,
+            'converge_tol_dz': 0.05, 'converge_tol_frac_TSE': 0., 'DEM_tol': None, 'repeat_dt': 1,
+            'Edit_only': False, 'dzdt_lags': None, 'prior_args': None, 'prior_edge_args': None,
+            'avg_scales': [], 'data_slope_sensors': None, 'E_slope_bias': 0.01, 'E_RMS_d2x_PS_bias': None,
+            'E_RMS_PS_bias': None, 'constraint_scaling_maps': None, 'error_res_scale': None, 'avg_masks': None,
+            'sigma_extra_masks': None, 'bias_nsigma_edit': None, 'bias_nsigma_iteration': 2,
+            'bias_edit_vals': None, 'sensor_grid_bias_params': None, 'ancillary_data': None,
+            'lagrangian_coords': None, 'z0_average_scale': None, 'erode_source_mask': True, 'VERBOSE': True,
+            'DEBUG': False,
+            # lssurf_amd solver options (new keys; defaults reproduce the exact LS solution to
+            # the tolerance documented in DESIGN.md §Parity)
+            'device': 0, 'lsq_atol': 1e-12, 'lsq_btol': 1e-12, 'lsq_conlim': 1e12, 'lsq_maxit': 0,
+            'lsq_precond': 1, 'lsq_warm_start': True}
+
+OUT_OF_SCOPE = ('bias_params', 'sensor_grid_bias_params', 'prior_args', 'prior_edge_args', 'lagrangian_coords',
+                'constraint_scaling_maps', 'mask_file', 'avg_masks', 'z0_average_scale', 'bias_edit_vals')
+
+
+class FitSystem:
+    """The device-resident smooth_fit system: G = [G_data; Gc] (unweighted COO -> device CSR),
+    Ip_c as a column map; rows re-weighted / re-selected per outer iteration."""
+
+    def __init__(self, G_data, Gc, keep_cols, n_full, device=0):
+        self.n_data, self.n_con = int(G_data.N_eq), int(Gc.N_eq)
+        self.keep_cols = keep_cols
+        self.n_full = int(n_full)
+        r1, c1, v1 = G_data.triplets()
+        r2, c2, v2 = Gc.triplets()
+        self.solver = LSQSolver(device)
+        self.solver.set_col_map(self.n_full, keep_cols)
+        self.solver.set_matrix_coo(self.n_data + self.n_con, self.n_full, np.concatenate([r1, r2 + self.n_data]),
+                                   np.concatenate([c1, c2]), np.concatenate([v1, v2]))
+        self.stats = None
+
+    def solve(self, row_weight, data_keep, rhs, x0=None, **opts):
+        keep = np.concatenate([np.asarray(data_keep, dtype=bool), np.ones(self.n_con, dtype=bool)])
+        self.solver.set_row_weight(row_weight)
+        self.solver.set_row_mask(keep)
+        x, self.stats = self.solver.solve(rhs, x0=x0, **opts)
+        return x
+
+    def expand(self, x):
+        m0 = np.zeros(self.n_full)
+        m0[self.keep_cols] = x
+        return m0
+
+    def data_forward(self, x):
+        """G_data · (Ip_c x), bit-identical to scipy's csr matvec of the reference."""
+        return self.solver.spmv(x)[:self.n_data]
+
+    def close(self):
+        self.solver.close()
+
+
+def check_data_against_DEM(in_TSE, data, m0, G_data, DEM_tol):
+    m1 = m0.copy()
+    m1[G_data.TOC['cols']['z0']] = 0
+    r_DEM = data.z - G_data.toCSR().dot(m1) - data.DEM
+    in_TSE[in_TSE] = np.abs(r_DEM[in_TSE]) < DEM_tol
+    return in_TSE
+
+
+def print_TOC(G_data, Gc):
+    print(f'G_data : \n\t{len(np.ravel(G_data.v)) / 1000}K values\n\t shape={np.array(G_data.shape) / 1000}K')
+    for label, op in (('G_data', G_data), ('Gc', Gc)):
+        print(label, 'rows:')
+        for name, rr in op.TOC['rows'].items():
+            print(f'\t{name}: {len(np.unique(rr)) / 1000}K')
+
+
+def _solve_opts(args):
+    return dict(atol=args['lsq_atol'], btol=args['lsq_btol'], conlim=args['lsq_conlim'], maxit=args['lsq_maxit'],
+                precond=args['lsq_precond'])
+
+
+def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grids, sigma_extra_masks=None):
+    """Outer editing loop (smooth_fit.py:100-210) around the device solve."""
+    in_TSE_original = np.zeros(data.shape, dtype=bool)
+    in_TSE_original[in_TSE] = True
+    N_editable = np.sum(data.editable) if 'editable' in data.fields else data.size
+    sigma_extra = np.zeros_like(data.z)
+    last_iteration = args['max_iterations'] <= 1
+    m0 = np.zeros(system.n_full)
+    x = None
+    rs_data = None
+    timing['lsq_iters'] = 0
+    for iteration in range(args['max_iterations']):
+        E2_plus = E_all ** 2
+        if last_iteration and args['sigma_extra_relax']:
+            if args['VERBOSE']:
+                print('smooth_fit.iterate_fit: relaxing errors by sigma_extra')
+            E2_plus[0:G_data.shape[0]] += sigma_extra ** 2
+        weight = 1. / np.sqrt(E2_plus)     # TCinv diagonal, smooth_fit.py:129
+        if args['VERBOSE']:
+            print('starting device lsqr solve for iteration %d at %s' % (iteration, ctime()), flush=True)
+        tic = time()
+        m0_last = m0
+        x0 = x if (args['lsq_warm_start'] and x is not None) else None
+        x = system.solve(weight, in_TSE, rhs, x0=x0, **_solve_opts(args))
+        m0 = system.expand(x)
+        timing['sparseqr_solve'] = time() - tic
+        timing['lsq_iters'] += int(system.stats['iters'])
+        timing['lsq_last'] = dict(system.stats)
+        r_data = data.z - system.data_forward(x)
+        rs_data = r_data / data.sigma
+        if last_iteration:
+            break
+        if args.get('sigma_extra_bin_spacing') is None:
+            sigma_extra = calc_sigma_extra(r_data, data.sigma, in_TSE, sigma_extra_masks)
+        else:
+            sigma_extra = calc_sigma_extra_on_grid(data.x, data.y, r_data, data.sigma, in_TSE,
+                                                   sigma_extra_masks=sigma_extra_masks,
+                                                   sigma_extra_max=args['sigma_extra_max'],
+                                                   spacing=args['sigma_extra_bin_spacing'])
+        sigma_aug = np.sqrt(data.sigma ** 2 + sigma_extra ** 2)
+        in_TSE_last = in_TSE
+        in_TSE = np.abs(r_data / sigma_aug) < 3.0
+        bias_editing_changed = False
+        if 'editable' in data.fields:
+            in_TSE[data.editable == 0] = in_TSE_original[data.editable == 0]
+        if args['DEM_tol'] is not None:
+            in_TSE = check_data_against_DEM(in_TSE, data, m0, G_data, args['DEM_tol'])
+        if not np.any(in_TSE):
+            if args['VERBOSE']:
+                print('Edited data empty, returning')
+            return m0, sigma_extra, in_TSE, rs_data
+        if np.max(np.abs((m0_last - m0)[Gc.TOC['cols']['dz']])) < args['converge_tol_dz'] and \
+                iteration > args['min_iterations']:
+            if args['VERBOSE']:
+                print('Solution identical to previous iteration with tolerance %3.1f, exiting after iteration %d'
+                      % (args['converge_tol_dz'], iteration))
+            last_iteration = True
+        if args['VERBOSE']:
+            print('found %d in TSE, dt=%3.0f' % (in_TSE.sum(), timing['sparseqr_solve']), flush=True)
+            if sigma_extra_masks is None:
+                print(f'\t median(sigma_extra)={np.median(sigma_extra):3.4f}')
+            else:
+                for key, ii in sigma_extra_masks.items():
+                    print(f'\t sigma_extra for {key} : {np.median(sigma_extra[ii]):3.4f}', flush=True)
+                for key, ii in sigma_extra_masks.items():
+                    print(f'\t sigma_hat for {key} : {RDE(r_data[ii] / sigma_aug[ii]):3.4f}', flush=True)
+        if iteration > 0 and iteration > args['bias_nsigma_iteration']:
+            frac_TSE_change = len(np.setxor1d(in_TSE_last, in_TSE)) / N_editable
+            if frac_TSE_change < args['converge_tol_frac_TSE']:
+                if args['VERBOSE']:
+                    print('filtering unchanged with tolerance %3.5f, will exit after iteration %d'
+                          % (args['converge_tol_frac_TSE'], iteration + 1))
+                last_iteration = True
+        if iteration >= np.maximum(args['min_iterations'], args['bias_nsigma_iteration'] + 1):
+            if np.all(sigma_extra < 0.5 * np.min(data.sigma[in_TSE])) and not bias_editing_changed:
+                if args['VERBOSE']:
+                    print('sigma_extra is small, performing one additional iteration', flush=True)
+                last_iteration = True
+        if iteration == args['max_iterations'] - 2:
+            last_iteration = True
+    return m0, sigma_extra, in_TSE, rs_data
+
+
+def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args):
+    """Output grids and fit statistics (smooth_fit.py:276-352)."""
+    z0g, dzg = grids['z0'], grids['dz']
+    m['z0'] = pc.grid.data().from_dict({'x': z0g.ctrs[1], 'y': z0g.ctrs[0], 'cell_area': z0g.cell_area,
+                                        'mask': z0g.mask, 'z0': np.reshape(m0[G_data.TOC['cols']['z0']], z0g.shape)})
+    m['dz'] = pc.grid.data().from_dict({'x': dzg.ctrs[1], 'y': dzg.ctrs[0], 'time': dzg.ctrs[2],
+                                        'dz': np.reshape(m0[G_data.TOC['cols']['dz']], dzg.shape),
+                                        'cell_area': dzg.cell_area, 'mask': dzg.mask})
+    for key, op in averaging_ops.items():
+        fields = {coord: ctr for coord, ctr in zip(op.dst_grid.coords, op.dst_grid.ctrs)}
+        fields.update({'cell_area': op.dst_grid.cell_area, key: op.grid_prod(m0)})
+        m[key] = pc.grid.data().from_dict(fields)
+    m['all'] = m0
+    m['extent'] = np.concatenate((z0g.bds[1], z0g.bds[0]))
+    m['sensor_bias_grids'] = {}
+    m['jitter_bias_grids'] = {}
+    Gc_csr = Gc.toCSR()
+    ru = Gc_csr.dot(m0)
+    rc = (1. / Ec) * ru          # TCinv_cov.dot(ru), smooth_fit.py:324-326
+    for eq_type in ['d2z_dt2', 'grad2_z0', 'grad2_dzdt', 'grad2_PS']:
+        if eq_type in Gc.TOC['rows']:
+            R[eq_type] = np.sum(rc[Gc.TOC['rows'][eq_type]] ** 2)
+            RMS[eq_type] = np.sqrt(np.mean(ru[Gc.TOC['rows'][eq_type]] ** 2))
+    tse = data.three_sigma_edit
+    r = (data.z - data.z_est)[tse]
+    if args['sigma_extra_relax']:
+        r_scaled = r / np.sqrt(data.sigma[tse] ** 2 + data.sigma_extra[tse] ** 2)
+    else:
+        r_scaled = r / data.sigma[tse]
+    Gd = G_data.toCSR()
+    for ff in ['dz', 'z0']:
+        Gsel = Gd[:, G_data.TOC['cols'][ff]][tse, :].T
+        count = Gsel.dot(np.ones_like(r)).reshape(grids[ff].shape)
+        m[ff].assign({'count': count})
+        m[ff].count[m[ff].count == 0] = np.nan
+        m[ff].assign({'misfit_scaled_rms': np.sqrt(Gsel.dot(r_scaled ** 2).reshape(grids[ff].shape) / m[ff].count)})
+        m[ff].assign({'misfit_rms': np.sqrt(Gsel.dot(r ** 2).reshape(grids[ff].shape) / m[ff].count)})
+
+
+def smooth_fit(**kwargs):
+    required = ('data', 'W', 'ctr', 'spacing', 'E_RMS')
+    args = dict(DEFAULTS)
+    args.update(kwargs)
+    for field in required:
+        if field not in kwargs:
+            raise ValueError('%s must be defined' % field)
+    for key in OUT_OF_SCOPE:
+        if args.get(key) is not None:
+            raise NotImplementedError(f'smooth_fit: {key!r} is outside lssurf_amd (SURVEY.md §2)')
+    if args.get('data_slope_sensors') is not None and len(args['data_slope_sensors']) > 0:
+        raise NotImplementedError("smooth_fit: 'data_slope_sensors' is outside lssurf_amd")
+    if args.get('avg_scales'):
+        raise NotImplementedError("smooth_fit: 'avg_scales' averaging products are the next §8 row")
+    if args.get('sigma_extra_keys') is not None:
+        raise NotImplementedError("smooth_fit: 'sigma_extra_keys' is outside lssurf_amd")
+
+    valid_data = np.isfinite(args['data'].z)
+    if 'sensor' not in args['data'].fields:
+        args['data'].assign(sensor=np.zeros(args['data'].shape))
+    timing = {}
+    m, E, R, RMS = {}, {}, {}, {}
+    tic = time()
+    grids, bds = setup_grids(args)
+    valid_data = valid_data & grids['dz'].validate_pts(args['data'].coords()) & \
+        grids['z0'].validate_pts(args['data'].coords()[0:2])
+    if not np.any(valid_data):
+        if args['VERBOSE']:
+            print('smooth_fit: no valid data')
+        return {'m': m, 'E': E, 'data': None, 'grids': grids, 'valid_data': valid_data, 'TOC': {}, 'R': {},
+                'RMS': {}, 'timing': timing, 'E_RMS': args['E_RMS']}
+    data = args['data'].copy_subset(valid_data)
+    validate_by_dz_mask(data, grids, valid_data)
+    if args['sigma_extra_masks'] is not None:
+        for key in args['sigma_extra_masks']:
+            args['sigma_extra_masks'][key] = args['sigma_extra_masks'][key][valid_data == 1]
+    if data.size == 0:
+        print('\tsmooth_fit.py: after masking, no data found')
+        return {'m': m, 'E': E, 'data': data, 'grids': grids, 'valid_data': valid_data, 'TOC': {}, 'R': {},
+                'RMS': {}, 'timing': timing, 'E_RMS': args['E_RMS']}
+
+    G_data = lin_op(grids['z0'], name='interp_z').interp_mtx(data.coords()[0:2])
+    G_data.add(lin_op(grids['dz'], name='interp_dz').interp_mtx(data.coords()))
+    constraint_op_list = []
+    if args['VERBOSE']:
+        print(f"smooth_fit: E_RMS={args['E_RMS']}")
+    setup_smoothness_constraints(grids, constraint_op_list, args['E_RMS'], args['mask_scale'])
+    for op in constraint_op_list:
+        if op.prior is None:
+            op.prior = np.zeros_like(op.expected)
+    Gc = lin_op(None, name='constraints').vstack(constraint_op_list)
+    N_eq = G_data.N_eq + Gc.N_eq
+    Ec = np.zeros(Gc.N_eq)
+    for op in constraint_op_list:
+        Ec[Gc.TOC['rows'][op.name]] = op.expected
+    Ed = data.sigma.ravel()
+    if np.any(Ed == 0):
+        raise ValueError('zero value found in data sigma')
+    if np.any(Ec == 0):
+        raise ValueError('zero value found in constraint sigma')
+    if args['DEBUG']:
+        print_TOC(G_data, Gc)
+    TCinv_diag = 1. / np.concatenate((Ed, Ec))
+    rhs = np.zeros([N_eq])
+    rhs[0:data.size] = data.z.ravel()
+    rhs[data.size:] = np.concatenate([op.prior for op in constraint_op_list])
+    keep_cols = reference_epoch_keep_cols(G_data.col_N, grids['dz'], args['reference_epoch'])
+    timing['setup'] = time() - tic
+    in_TSE = data.three_sigma_edit > 0.01 if 'three_sigma_edit' in data.fields else np.ones(G_data.N_eq, dtype=bool)
+    if args['VERBOSE']:
+        print('initial: %d:' % np.max(G_data.r), flush=True)
+    if args['return_fit_objects']:
+        return {'data': data, 'G_data': G_data, 'Gc': Gc, 'grids': grids, 'Ed': Ed, 'Ec': Ec}
+
+    system = None
+    try:
+        if args['max_iterations'] > 0:
+            tic = time()
+            system = FitSystem(G_data, Gc, keep_cols, Gc.col_N, device=args['device'])
+            timing['device_setup'] = time() - tic
+            tic_iteration = time()
+            m0, sigma_extra, in_TSE, rs_data = iterate_fit(data, system, rhs, 1. / TCinv_diag, G_data, Gc, in_TSE,
+                                                           timing, args, grids,
+                                                           sigma_extra_masks=args['sigma_extra_masks'])
+            timing['iteration'] = time() - tic_iteration
+            valid_data[valid_data] = in_TSE
+            data.assign({'three_sigma_edit': in_TSE})
+            data.assign({'sigma_extra': sigma_extra})
+            data.assign({'z_est': np.reshape(system.data_forward(m0[keep_cols]), data.shape)})
+            if args['mask_update_function'] is not None:
+                averaging_ops = {}
+                parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args)
+                args['mask_update_function'](grids, m, args)
+            averaging_ops = setup_averaging_ops(grids['dz'], grids['dz'].col_N, args, grids['dz'].cell_area)
+            averaging_ops.update(setup_z0_avg(grids, grids['dz'].col_N, args))
+            averaging_ops.update(setup_avg_mask_ops(grids['dz'], G_data.col_N, args['avg_masks'], args['dzdt_lags']))
+            parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args)
+            tse = data.three_sigma_edit == 1
+            r_data = data.z_est[tse] - data.z[tse]
+            R['data'] = np.sum((r_data / data.sigma[tse]) ** 2)
+            RMS['data'] = np.sqrt(np.mean(r_data ** 2))
+        else:
+            averaging_ops = setup_averaging_ops(grids['dz'], grids['dz'].col_N, args, grids['dz'].cell_area)
+        if args['compute_E']:
+            from .errors import calc_and_parse_errors
+            if 'sigma_extra' not in data.fields:
+                data.assign({'sigma_extra': np.zeros_like(data.sigma)})
+                tse = data.three_sigma_edit == 1
+                r_data = data.z_est[tse] - data.z[tse]
+                data.sigma_extra[tse] = calc_sigma_extra(r_data, data.sigma[tse], np.ones(tse.sum(), dtype=bool))
+            if args['VERBOSE']:
+                print('Starting uncertainty calculation', flush=True)
+                tic_error = time()
+            calc_and_parse_errors(E, G_data, Gc, Ed, Ec, data, in_TSE, keep_cols, grids, averaging_ops,
+                                  device=args['device'], timing=timing)
+            if args['VERBOSE']:
+                print('\tUncertainty propagation took %3.2f seconds' % (time() - tic_error), flush=True)
+    finally:
+        if system is not None:
+            system.close()
+    return {'m': m, 'E': E, 'data': data, 'grids': grids, 'valid_data': valid_data, 'TOC': Gc.TOC, 'R': R,
+            'RMS': RMS, 'timing': timing, 'E_RMS': args['E_RMS'], 'dzdt_lags': args['dzdt_lags']}
+
+
+# re-exported for callers that build Ip_c explicitly (smooth_fit.py:624)
+__all__ = ['smooth_fit', 'iterate_fit', 'parse_model', 'FitSystem', 'build_reference_epoch_matrix',
+           'check_data_against_DEM']

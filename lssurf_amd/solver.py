@@ -1,0 +1,179 @@
+"""Host mirror of the solve boundary: a handle on one MI355X holding the formed least-squares
+system, plus drop-ins for the reference's Cython triangular kernels.
+
+* ``LSQSolver``  — replaces ``sparseqr.solve`` (LSsurf/smooth_fit.py:142) and the residual
+  products ``G_data.toCSR().dot(m0)`` (smooth_fit.py:146,662).  The COO triplets of the
+  unweighted operator, the column map Ip_c, the row weights (TCinv) and the row selection Ip_r
+  go to the device once; outer iterations only change weights / masks.
+* ``inv_tr_upper``, ``propagate_qz_errors``, ``spsolve_tr_upper`` — same signatures and
+  outputs as LSsurf/inv_tr_upper.pyx:19, propagate_qz_errors.pyx:15, spsolve_tr_upper.pyx:11,
+  computed by liblsqsurf's HIP kernels.
+"""
+import ctypes
+
+import numpy as np
+import scipy.sparse as sp
+
+from ._native import LsqStats, NativeError, as_c, default_opts, load, ptr
+
+
+class LSQSolver:
+    """One device-resident least-squares system ``min || diag(w)·mask·(G x − b) ||``."""
+
+    def __init__(self, device=0):
+        self._L = load()
+        self._h = self._L.lsq_create(int(device))
+        if not self._h:
+            raise NativeError(f'lsq_create({device}) failed: no gfx950 (MI355X) device visible')
+        self.device = device
+        self.m = self.n = self.n_full = None
+
+    # ---- lifetime --------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, '_h', None):
+            self._L.lsq_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc, what):
+        if rc < 0:
+            raise NativeError(f'{what}: {self._L.lsq_last_error(self._h).decode()}')
+        return rc
+
+    # ---- formation ---------------------------------------------------------------------------
+    def set_col_map(self, n_full, keep_cols):
+        keep = as_c(keep_cols, np.int64)
+        self._check(self._L.lsq_set_col_map(self._h, int(n_full), ptr(keep), keep.size), 'lsq_set_col_map')
+        self.n = keep.size
+        self.n_full = int(n_full)
+
+    def set_matrix_coo(self, m, n_full, r, c, v, row_weight=None):
+        r, c, v = as_c(r, np.int64).ravel(), as_c(c, np.int64).ravel(), as_c(v, np.float64).ravel()
+        w = None if row_weight is None else as_c(row_weight, np.float64)
+        self._check(self._L.lsq_set_matrix_coo(self._h, int(m), int(n_full), v.size, ptr(r), ptr(c), ptr(v), ptr(w)),
+                    'lsq_set_matrix_coo')
+        self.m = int(m)
+        if self.n is None:
+            self.n = int(n_full)
+        self.n_full = int(n_full)
+
+    def set_row_weight(self, w):
+        w = None if w is None else as_c(w, np.float64)
+        self._check(self._L.lsq_set_row_weight(self._h, ptr(w)), 'lsq_set_row_weight')
+
+    def set_row_mask(self, keep):
+        k = None if keep is None else as_c(np.asarray(keep, dtype=bool), np.uint8)
+        self._check(self._L.lsq_set_row_mask(self._h, ptr(k)), 'lsq_set_row_mask')
+
+    def shape(self):
+        m, n, z = (ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64())
+        self._check(self._L.lsq_shape(self._h, ctypes.byref(m), ctypes.byref(n), ctypes.byref(z)), 'lsq_shape')
+        return m.value, n.value, z.value
+
+    def get_csr(self):
+        """The formed A = Ip_r·TCinv·G·Ip_c (selected rows), as scipy CSR."""
+        m, n, z = self.shape()
+        rp = np.zeros(m + 1, np.int64)
+        ci = np.zeros(max(z, 1), np.int32)
+        v = np.zeros(max(z, 1))
+        self._check(self._L.lsq_get_csr(self._h, ptr(rp), ptr(ci), ptr(v)), 'lsq_get_csr')
+        return sp.csr_matrix((v[:z], ci[:z], rp), shape=(m, n))
+
+    # ---- solve -------------------------------------------------------------------------------
+    def solve(self, b, x0=None, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, batch=16,
+              use_graph=True):
+        """LSQR; returns (x, stats) with scipy-lsqr-style stats (iters, istop, r1norm, ...)."""
+        b = as_c(b, np.float64)
+        if b.size != self.m:
+            raise ValueError(f'b has {b.size} rows, system has {self.m}')
+        x = np.zeros(self.n) if x0 is None else as_c(x0, np.float64).copy()
+        o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond),
+                         use_x0=int(x0 is not None), batch=int(batch), use_graph=int(bool(use_graph)))
+        st = LsqStats()
+        self._check(self._L.lsq_solve(self._h, ptr(b), ptr(x), ctypes.byref(o), ctypes.byref(st)), 'lsq_solve')
+        return x, st.as_dict()
+
+    def iterate(self, b, iters, precond=1, batch=16, use_graph=True):
+        b = as_c(b, np.float64)
+        o = default_opts(precond=int(precond), batch=int(batch), use_graph=int(bool(use_graph)))
+        st = LsqStats()
+        self._check(self._L.lsq_iterate(self._h, ptr(b), int(iters), ctypes.byref(o), ctypes.byref(st)),
+                    'lsq_iterate')
+        return st.as_dict()
+
+    def profile_kernels(self, reps=20):
+        ms = np.zeros(4)
+        self._check(self._L.lsq_profile_kernels(self._h, int(reps), ptr(ms)), 'lsq_profile_kernels')
+        return dict(zip(['xw_spmv', 'spmtv', 'beta', 'givens'], ms.tolist()))
+
+    def info(self):
+        o = np.zeros(6, np.int64)
+        self._check(self._L.lsq_sell_info(self._h, ptr(o)), 'lsq_sell_info')
+        return dict(zip(['m', 'n', 'nnz', 'sell_A', 'sell_AT', 'device_bytes'], o.tolist()))
+
+    def spmv(self, x, trans=False):
+        """G x (trans False) or Gᵀ x on the UNWEIGHTED formed operator, all rows."""
+        x = as_c(x, np.float64)
+        nout = self.n if trans else self.m
+        y = np.zeros(nout)
+        self._check(self._L.lsq_spmv(self._h, int(bool(trans)), ptr(x), ptr(y)), 'lsq_spmv')
+        return y
+
+
+# ---- triangular kernels (drop-in signatures of the reference's Cython modules) -------------
+def _tri_csr(R):
+    R = sp.csr_matrix(R)
+    if R.shape[0] != R.shape[1]:
+        raise ValueError('R must be square')
+    return (R.shape[0], as_c(R.indptr, np.int32), as_c(R.indices, np.int32), as_c(R.data, np.float64))
+
+
+def _tri_check(L, rc, what):
+    if rc < 0:
+        raise NativeError(f'{what}: {L.tri_last_error().decode()}')
+    return rc
+
+
+def inv_tr_upper(R, nnz, tol, device=0):
+    """LSsurf/inv_tr_upper.pyx:19 — returns (rows, cols, vals, status), same order and values."""
+    L = load()
+    N, rp, ci, v = _tri_csr(R)
+    nnz = int(nnz)
+    rr = np.zeros(nnz, np.int32)
+    cc = np.zeros(nnz, np.int32)
+    vv = np.zeros(nnz)
+    n_out = ctypes.c_int64()
+    st = _tri_check(L, L.tri_upper_inv_csr(device, N, ptr(rp), ptr(ci), ptr(v), nnz, ctypes.c_float(tol), ptr(rr),
+                                           ptr(cc), ptr(vv), ctypes.byref(n_out)), 'tri_upper_inv_csr')
+    k = n_out.value
+    return rr[:k], cc[:k], vv[:k], st
+
+
+def propagate_qz_errors(R, device=0):
+    """LSsurf/propagate_qz_errors.pyx:15 — row RSS of R^-1."""
+    L = load()
+    N, rp, ci, v = _tri_csr(R)
+    E = np.zeros(N)
+    _tri_check(L, L.tri_upper_rowrss_csr(device, N, ptr(rp), ptr(ci), ptr(v), ptr(E)), 'tri_upper_rowrss_csr')
+    return E
+
+
+def spsolve_tr_upper(A, b, device=0):
+    """LSsurf/spsolve_tr_upper.pyx:11 — x = A^-1 b for upper-triangular CSR A."""
+    L = load()
+    N, rp, ci, v = _tri_csr(A)
+    b = as_c(b, np.float64)
+    x = np.zeros(N)
+    _tri_check(L, L.tri_upper_solve_csr(device, N, ptr(rp), ptr(ci), ptr(v), ptr(b), ptr(x)), 'tri_upper_solve_csr')
+    return x

@@ -1,0 +1,94 @@
+"""ctypes wrappers for the oracle's C restatements (TEST INFRASTRUCTURE ONLY).
+
+build() compiles oracle/lsqr_cpu.c + oracle/tri_upper.c into oracle/_cpu.so with gcc -O2
+-fopenmp (no -march: plain SSE2 doubles, no FMA — matching the reference's Cython build).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import scipy.sparse as sp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, '_cpu.so')
+SRC = [os.path.join(HERE, 'lsqr_cpu.c'), os.path.join(HERE, 'tri_upper.c')]
+_lib = None
+
+
+def build(force=False):
+    if not force and os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(s) for s in SRC):
+        return LIB
+    cmd = ['gcc', '-O2', '-fopenmp', '-fPIC', '-shared', '-ffp-contract=off', '-o', LIB, *SRC, '-lm']
+    subprocess.run(cmd, check=True)
+    return LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB)
+        P = ctypes.c_void_p
+        i64, i32, f64, f32 = ctypes.c_int64, ctypes.c_int32, ctypes.c_double, ctypes.c_float
+        L.lsqr_cpu.argtypes = [i64, i64, P, P, P, P, P, f64, f64, f64, i64, ctypes.c_int, i64, ctypes.c_int, P]
+        L.lsqr_cpu.restype = ctypes.c_int
+        L.oracle_inv_tr_upper.argtypes = [i64, P, P, P, i64, f32, P, P, P, P]
+        L.oracle_inv_tr_upper.restype = ctypes.c_int
+        L.oracle_propagate_qz_errors.argtypes = [i64, P, P, P, P]
+        L.oracle_spsolve_tr_upper.argtypes = [i64, P, P, P, P, P]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _csr(A):
+    A = sp.csr_matrix(A)
+    rp = np.ascontiguousarray(A.indptr, dtype=np.int64)
+    ci = np.ascontiguousarray(A.indices, dtype=np.int32)
+    v = np.ascontiguousarray(A.data, dtype=np.float64)
+    return A.shape, rp, ci, v
+
+
+def lsqr(A, b, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, fixed_iters=0, threads=0):
+    """CPU LSQR on the final weighted A; returns (x, stats dict)."""
+    (m, n), rp, ci, v = _csr(A)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    x = np.zeros(n)
+    st = np.zeros(10)
+    lib().lsqr_cpu(m, n, _p(rp), _p(ci), _p(v), _p(b), _p(x), atol, btol, conlim, maxit, precond, fixed_iters,
+                   threads, _p(st))
+    keys = ['iters', 'istop', 'r1norm', 'r2norm', 'anorm', 'acond', 'arnorm', 'xnorm', 'time_s', 'threads']
+    return x, dict(zip(keys, st.tolist()))
+
+
+def inv_tr_upper(R, nnz, tol):
+    (N, _), rp, ci, v = _csr(R)
+    rp = rp.astype(np.int32)
+    rr = np.zeros(nnz, np.int32)
+    cc = np.zeros(nnz, np.int32)
+    vv = np.zeros(nnz)
+    n_out = np.zeros(1, np.int64)
+    st = lib().oracle_inv_tr_upper(N, _p(rp), _p(ci), _p(v), nnz, tol, _p(rr), _p(cc), _p(vv), _p(n_out))
+    k = int(n_out[0])
+    return rr[:k], cc[:k], vv[:k], st
+
+
+def propagate_qz_errors(R):
+    (N, _), rp, ci, v = _csr(R)
+    rp = rp.astype(np.int32)
+    E = np.zeros(N)
+    lib().oracle_propagate_qz_errors(N, _p(rp), _p(ci), _p(v), _p(E))
+    return E
+
+
+def spsolve_tr_upper(R, b):
+    (N, _), rp, ci, v = _csr(R)
+    rp = rp.astype(np.int32)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    x = np.zeros(N)
+    lib().oracle_spsolve_tr_upper(N, _p(rp), _p(ci), _p(v), _p(b), _p(x))
+    return x
