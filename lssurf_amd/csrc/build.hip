@@ -286,6 +286,10 @@ void build_sell(Sell& S, const Csr& C, hipStream_t st) {
     S.nent = exclusive_scan_i64(S.sp.p, S.nslices + 1, st);
     S.ci.alloc(std::max<int64_t>(S.nent, 1));
     S.val.alloc(std::max<int64_t>(S.nent, 1));
+    // lanes past the last row of the final slice are never written by k_sell_cols/k_sell_vals:
+    // give them column 0 and value 0 so any read of them is in bounds and contributes nothing
+    S.ci.zero(st);
+    S.val.zero(st);
     hipLaunchKernelGGL(k_sell_cols, dim3(grid_for(C.m)), dim3(BLOCK), 0, st, C.m, C.rp.p, C.ci.p, S.sp.p, S.ci.p);
     KERNEL_CHECK();
 }

@@ -65,7 +65,7 @@ __global__ __launch_bounds__(BLOCK) void k_init_u(int64_t m, int64_t nslices, co
     for (int64_t s = (int64_t)blockIdx.x * 4 + wid; s < nslices; s += (int64_t)gridDim.x * 4) {
         const int64_t row = s * SELL_C + lane;
         double ax = 0.0;
-        if (y0) {
+        if (y0 && row < m) {
             const int64_t base = sp[s];
             ax = sell_row_dot(ci, val, base, (sp[s + 1] - base) / SELL_C, lane, y0);
         }
@@ -110,10 +110,10 @@ __global__ __launch_bounds__(BLOCK) void k_xw_spmv(const LsqState* __restrict__ 
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     double su = 0.0;
     for (int64_t s = (int64_t)bid * 4 + wid; s < nslices; s += (int64_t)gA * 4) {
-        const int64_t base = sp[s];
-        const double ax = sell_row_dot(ci, val, base, (sp[s + 1] - base) / SELL_C, lane, vt);
         const int64_t row = s * SELL_C + lane;
         if (row < m) {
+            const int64_t base = sp[s];
+            const double ax = sell_row_dot(ci, val, base, (sp[s + 1] - base) / SELL_C, lane, vt);
             const double un = ax * ia - alpha * (u[row] * ib);
             u[row] = un;
             su += un * un;
@@ -138,10 +138,12 @@ __global__ __launch_bounds__(BLOCK) void k_spmtv(const LsqState* __restrict__ st
         double vn;
         if (skip) {
             vn = row < n ? vin[row] : 0.0;
-        } else {
+        } else if (row < n) {
             const int64_t base = sp[s];
             const double atu = sell_row_dot(ci, val, base, (sp[s + 1] - base) / SELL_C, lane, u);
-            vn = row < n ? atu * ib - beta * (vin[row] * ia) : 0.0;
+            vn = atu * ib - beta * (vin[row] * ia);
+        } else {
+            vn = 0.0;
         }
         if (row < n) {
             vout[row] = vn;

@@ -1,0 +1,46 @@
+"""Synthetic point clouds for the BASELINE.json configurations.
+
+Domain W_x = W_y = (n-1)*100 m centred on 0, spacing z0 = dz = 100 m, dt = 0.25,
+W_t = (nt-1)*0.25, reference_epoch = nt//2; points uniform in (x, y, t) from
+default_rng(20251121 + config_id); z = 10 sin(2πx/Lx) cos(2πy/Ly) + 0.5 t exp(-r²/(W/4)²)
++ N(0, 0.1), Lx = W/2, Ly = W/3, sigma = 0.1; E_RMS = notebook cell-17 set.
+"""
+import numpy as np
+
+from . import containers as pc
+
+E_RMS_NOTEBOOK = {'d2z0_dx2': 0.03, 'dz0_dx': 75., 'd3z_dx2dt': 0.006, 'd2z_dxdt': 15., 'd2z_dt2': 5000.}
+E_RMS_STIFF = {'d2z0_dx2': 0.0006, 'dz0_dx': 0.9, 'd3z_dx2dt': 1e-4, 'd2z_dxdt': 0.15, 'd2z_dt2': 0.5}
+
+# id: (nodes per side, epochs, points)   — BASELINE.json configs (C1 is the notebook-scale case)
+CONFIGS = {
+    'c1': (128, 9, 10_000),
+    'c3': (512, 12, 1_000_000),
+    'c4': (1024, 12, 2_000_000),
+    'c5': (2048, 12, 8_000_000),
+    # small ones for tests / smoke
+    't64': (64, 12, 8_192),
+    't256': (256, 12, 131_072),
+}
+
+
+def config_kwargs(name, stiff=False):
+    n, nt, npts = CONFIGS[name]
+    W = {'x': (n - 1) * 100., 'y': (n - 1) * 100., 't': (nt - 1) * 0.25}
+    return dict(W=W, ctr={'x': 0., 'y': 0., 't': 0.}, spacing={'z0': 100., 'dz': 100., 'dt': 0.25},
+                E_RMS=dict(E_RMS_STIFF if stiff else E_RMS_NOTEBOOK), reference_epoch=nt // 2), npts
+
+
+def points(name, config_id=None):
+    kw, npts = config_kwargs(name)
+    cid = list(CONFIGS).index(name) if config_id is None else config_id
+    rng = np.random.default_rng(20251121 + cid)
+    W, ctr = kw['W'], kw['ctr']
+    x = ctr['x'] + (rng.random(npts) - 0.5) * W['x']
+    y = ctr['y'] + (rng.random(npts) - 0.5) * W['y']
+    t = ctr['t'] + (rng.random(npts) - 0.5) * W['t']
+    Lx, Ly = W['x'] / 2, W['y'] / 3
+    z = 10 * np.sin(2 * np.pi * x / Lx) * np.cos(2 * np.pi * y / Ly) \
+        + 0.5 * t * np.exp(-((x - ctr['x']) ** 2 + (y - ctr['y']) ** 2) / (W['x'] / 4) ** 2) \
+        + rng.normal(0, 0.1, npts)
+    return pc.data().from_dict({'x': x, 'y': y, 'time': t, 'z': z, 'sigma': np.full(npts, 0.1)}), kw

@@ -1,0 +1,55 @@
+"""The C-ABI library loads and exports every symbol include/*.h declares (no compute calls:
+this runs without a GPU)."""
+import ctypes
+import glob
+import os
+import re
+
+from conftest import ROOT
+
+
+def _declared():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, 'include', '*.h')):
+        text = open(h).read()
+        text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
+        for m in re.finditer(r'^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b([a-z_][a-z0-9_]*)\s*\(', text, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_header_declares_the_boundary():
+    names = _declared()
+    for required in ('lsq_create', 'lsq_set_matrix_coo', 'lsq_solve', 'lsq_spmv', 'tri_upper_inv_csr',
+                     'tri_upper_rowrss_csr', 'tri_upper_solve_csr'):
+        assert required in names
+
+
+def test_library_exports_every_declared_symbol():
+    from lssurf_amd import _native
+    if not os.path.exists(_native.LIB_PATH):
+        from lssurf_amd import build
+        build.build()
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    missing = [n for n in _declared() if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(_native.EXPORTS) == _declared()
+
+
+def test_no_gpu_create_fails_loudly():
+    """Without a gfx950 device the product path raises instead of falling back to the CPU."""
+    import pytest
+    from lssurf_amd import _native
+    from lssurf_amd.solver import LSQSolver
+    lib = _native.load()
+    n = ctypes.c_int()
+    try:
+        import torch
+        has_gpu = torch.cuda.is_available()
+    except Exception:   # noqa: BLE001
+        has_gpu = False
+    if has_gpu:
+        pytest.skip('a GPU is present')
+    with pytest.raises(_native.NativeError):
+        LSQSolver(0)
+    assert lib is not None and n.value == 0

@@ -1,0 +1,195 @@
+"""GPU parity of the solve path (through liblsqsurf's C ABI): device formation must equal the
+reference's matrix bit-for-bit; LSQR must reach the exact LS solution within the stated
+tolerance (||x-x*||/||x*|| <= 1e-6 and max|x-x*| <= 1e-4 m; the defaults
+reach ~1e-9)."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import lssurf_amd as LS
+from conftest import SYSTEMS, golden, golden_csr, golden_kwargs, golden_points
+from lssurf_amd.constraint_functions import reference_epoch_keep_cols
+from lssurf_amd.smooth_fit import FitSystem
+from oracle import cpu, dense
+
+pytestmark = pytest.mark.gpu
+REL, ABS = 1e-6, 1e-4
+
+
+def _fit_system(name):
+    g = golden(f'sys_{name}.npz')
+    kw = golden_kwargs(g)
+    S = LS.smooth_fit(data=golden_points(g), return_fit_objects=True, **kw)
+    keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch'])
+    sysm = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N)
+    E_all = 1 / (1. / np.concatenate((S['Ed'], S['Ec'])))
+    w = 1. / np.sqrt(E_all ** 2)
+    rhs = np.zeros(S['G_data'].N_eq + S['Gc'].N_eq)
+    rhs[:S['data'].size] = S['data'].z
+    return g, S, sysm, w, rhs
+
+
+@pytest.mark.parametrize('name', SYSTEMS)
+def test_device_formation_bitwise(gpu_available, name):
+    g, S, sysm, w, rhs = _fit_system(name)
+    sysm.solver.set_row_weight(w)
+    sysm.solver.set_row_mask(np.ones(sysm.n_data + sysm.n_con, bool))
+    A = sysm.solver.get_csr()
+    ref = golden_csr(g)
+    sysm.close()
+    assert A.shape == ref.shape
+    np.testing.assert_array_equal(A.indptr, ref.indptr)
+    np.testing.assert_array_equal(A.indices, ref.indices)
+    np.testing.assert_array_equal(A.data, ref.data)
+
+
+@pytest.mark.parametrize('name', SYSTEMS)
+def test_lsqr_matches_exact_solution(gpu_available, name):
+    g, S, sysm, w, rhs = _fit_system(name)
+    x = sysm.solve(w, np.ones(sysm.n_data, bool), rhs, atol=1e-12, btol=1e-12, conlim=1e12)
+    st = sysm.stats
+    sysm.close()
+    xs = g['x']
+    assert st['istop'] in (1, 2), st
+    assert np.linalg.norm(x - xs) / np.linalg.norm(xs) <= REL
+    assert np.max(np.abs(x - xs)) <= ABS
+
+
+@pytest.mark.parametrize('name', ['sf3d', 'nb_xt'])
+def test_spmv_bitwise_vs_scipy(gpu_available, name):
+    g, S, sysm, w, rhs = _fit_system(name)
+    rng = np.random.default_rng(1)
+    x = rng.normal(size=sysm.solver.n)
+    y = sysm.solver.spmv(x)
+    yt = sysm.solver.spmv(rng.normal(size=sysm.solver.m), trans=True)
+    sysm.close()
+    G = sp.vstack([S['G_data'].toCSR(), S['Gc'].toCSR()]).tocsr()
+    G = sp.csr_matrix(G[:, sysm.keep_cols])
+    G.sort_indices()
+    np.testing.assert_array_equal(y, G.dot(x))
+    assert yt.shape == (sysm.solver.n,)
+
+
+def test_gpu_cpu_lsqr_agree(gpu_available):
+    g = golden('sys_sf3d.npz')
+    A = golden_csr(g)
+    with LS.LSQSolver(0) as s:
+        coo = A.tocoo()
+        s.set_matrix_coo(A.shape[0], A.shape[1], coo.row, coo.col, coo.data)
+        xg, stg = s.solve(g['b'], atol=1e-12, btol=1e-12, conlim=1e12)
+    xc, stc = cpu.lsqr(A, g['b'], atol=1e-12, btol=1e-12, conlim=1e12)
+    assert abs(stg['iters'] - stc['iters']) <= max(5, 0.05 * stc['iters'])
+    assert np.linalg.norm(xg - xc) / np.linalg.norm(xc) < 1e-9
+
+
+def test_row_mask_equals_row_removal(gpu_available):
+    rng = np.random.default_rng(3)
+    A = sp.random(400, 60, density=0.08, random_state=rng, format='csr') + sp.eye(400, 60)
+    b = rng.normal(size=400)
+    keep = rng.random(400) > 0.3
+    w = rng.uniform(0.5, 2.0, 400)
+    coo = A.tocoo()
+    with LS.LSQSolver(0) as s:
+        s.set_matrix_coo(400, 60, coo.row, coo.col, coo.data, row_weight=w)
+        s.set_row_mask(keep)
+        x1, _ = s.solve(b, atol=1e-13, btol=1e-13, conlim=1e14)
+        Am = s.get_csr()
+    Aref = sp.diags(w[keep]) @ A[keep]
+    Aref = sp.csr_matrix(Aref)
+    Aref.sort_indices()
+    np.testing.assert_array_equal(Am.indices, Aref.indices)
+    np.testing.assert_array_equal(Am.data, Aref.data)
+    xs = dense.ls_solve_dense(Aref, w[keep] * b[keep])
+    assert np.linalg.norm(x1 - xs) / np.linalg.norm(xs) < 1e-9
+
+
+def test_duplicates_zeros_and_colmap(gpu_available):
+    """toCSR semantics: drop v == 0, sum duplicates, drop zero sums, remove Ip_c columns."""
+    rng = np.random.default_rng(4)
+    m, n = 50, 30
+    r = np.r_[rng.integers(0, m, 300), 5, 5, 5, 7, 7, 9]
+    c = np.r_[rng.integers(0, n, 300), 3, 3, 3, 4, 4, 10**6]   # 3 dups, a cancelling pair, a bad col with v=0
+    v = np.r_[rng.normal(size=300), 0.25, 0.5, 0.125, 1.5, -1.5, 0.0]
+    v[::17] = 0.0
+    keep_cols = np.setdiff1d(np.arange(n), [2, 11, 29])
+    with LS.LSQSolver(0) as s:
+        s.set_col_map(n, keep_cols)
+        s.set_matrix_coo(m, n, r, c, v)     # the out-of-range column carries v == 0: ignored
+        A = s.get_csr()
+    nz = v != 0
+    ref = sp.csr_matrix((v[nz], (r[nz], c[nz])), shape=(m, n))[:, keep_cols]
+    ref = sp.csr_matrix(ref)
+    ref.eliminate_zeros()
+    ref.sort_indices()
+    np.testing.assert_array_equal(A.indptr, ref.indptr)
+    np.testing.assert_array_equal(A.indices, ref.indices)
+    np.testing.assert_allclose(A.data, ref.data, rtol=1e-15)
+
+
+def test_bad_index_raises(gpu_available):
+    with LS.LSQSolver(0) as s:
+        with pytest.raises(LS.solver.NativeError):
+            s.set_matrix_coo(4, 4, np.array([0, 9]), np.array([0, 1]), np.array([1.0, 1.0]))
+
+
+def test_warm_start_and_zero_rhs(gpu_available):
+    g = golden('sys_lin2d.npz')
+    A = golden_csr(g)
+    coo = A.tocoo()
+    with LS.LSQSolver(0) as s:
+        s.set_matrix_coo(A.shape[0], A.shape[1], coo.row, coo.col, coo.data)
+        x, st = s.solve(g['b'], atol=1e-12, btol=1e-12)
+        x2, st2 = s.solve(g['b'], x0=x, atol=1e-12, btol=1e-12)
+        z, stz = s.solve(np.zeros(A.shape[0]))
+        x3, st3 = s.solve(g['b'], precond=0, atol=1e-12, btol=1e-12, conlim=1e14, maxit=20000)
+        st_it = s.iterate(g['b'], 37)
+    assert st2['iters'] < st['iters'] / 4
+    assert np.linalg.norm(x2 - g['x']) / np.linalg.norm(g['x']) < 1e-8
+    assert np.all(z == 0) and stz['iters'] == 0
+    assert np.linalg.norm(x3 - g['x']) / np.linalg.norm(g['x']) < 1e-6
+    assert st_it['iters'] == 37
+
+
+def test_sparseqr_compat_solve(gpu_available):
+    from lssurf_amd import sparseqr_compat as sparseqr
+    g = golden('sys_lin2d.npz')
+    x = sparseqr.solve(golden_csr(g).tocoo(), g['b'])
+    assert x.ndim == 1
+    assert np.linalg.norm(x - g['x']) / np.linalg.norm(g['x']) < 1e-8
+
+
+def test_medium_system_formation_and_solve(gpu_available):
+    """A 48x48x8 problem (bigger than the dense oracle likes): device formation == scipy
+    formation bitwise; GPU LSQR == CPU oracle LSQR."""
+    from lssurf_amd import containers as pc
+    rng = np.random.default_rng(11)
+    W = {'x': 4700., 'y': 4700., 't': 1.75}
+    ctr = {'x': 0., 'y': 0., 't': 0.}
+    n = 9000
+    x = (rng.random(n) - .5) * W['x']
+    y = (rng.random(n) - .5) * W['y']
+    t = (rng.random(n) - .5) * W['t']
+    z = 10 * np.sin(2 * np.pi * x / 2000) + t + rng.normal(0, .1, n)
+    D = pc.data().from_dict({'x': x, 'y': y, 'time': t, 'z': z, 'sigma': np.full(n, .1)})
+    kw = dict(W=W, ctr=ctr, spacing={'z0': 100., 'dz': 100., 'dt': .25},
+              E_RMS={'d2z0_dx2': 0.03, 'dz0_dx': 75., 'd3z_dx2dt': 0.006, 'd2z_dxdt': 15., 'd2z_dt2': 5000.},
+              reference_epoch=3, VERBOSE=False)
+    S = LS.smooth_fit(data=D, return_fit_objects=True, **kw)
+    keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], 3)
+    sysm = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N)
+    E_all = 1 / (1. / np.concatenate((S['Ed'], S['Ec'])))
+    wgt = 1. / np.sqrt(E_all ** 2)
+    rhs = np.zeros(wgt.size)
+    rhs[:S['data'].size] = S['data'].z
+    xg = sysm.solve(wgt, np.ones(sysm.n_data, bool), rhs, atol=1e-12, btol=1e-12, conlim=1e12)
+    A = sysm.solver.get_csr()
+    sysm.close()
+    N_eq = wgt.size
+    G = sp.vstack([S['G_data'].toCSR(), S['Gc'].toCSR()]).tocoo()
+    G = G.dot(LS.build_reference_epoch_matrix(S['G_data'], S['Gc'], S['grids'], 3))
+    Aref = sp.csr_matrix(sp.dia_matrix((wgt, 0), shape=(N_eq, N_eq)).dot(G))
+    Aref.sort_indices()
+    np.testing.assert_array_equal(A.indices, Aref.indices)
+    np.testing.assert_array_equal(A.data, Aref.data)
+    xc, stc = cpu.lsqr(Aref, wgt * rhs, atol=1e-12, btol=1e-12, conlim=1e12)
+    assert np.linalg.norm(xg - xc) / np.linalg.norm(xc) < 1e-8

@@ -1,0 +1,65 @@
+"""End-to-end smooth_fit on the GPU vs the reference's outputs (reference run with an exact LS
+solve) and the notebook's analytic amplitude KAT."""
+import numpy as np
+import pytest
+
+import lssurf_amd as LS
+from conftest import golden, golden_kwargs, golden_points
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    ok = np.isfinite(b)
+    return np.linalg.norm(a[ok] - b[ok]) / max(np.linalg.norm(b[ok]), 1e-300)
+
+
+@pytest.mark.parametrize('name', ['sf3d', 'nb_xt'])
+def test_single_iteration_outputs(gpu_available, name):
+    g = golden(f'sys_{name}.npz')
+    S = LS.smooth_fit(data=golden_points(g), **golden_kwargs(g))
+    m = S['m']
+    assert _rel(m['z0'].z0, g['z0']) < 1e-6
+    assert _rel(m['dz'].dz, g['dz']) < 1e-6
+    assert np.max(np.abs(m['dz'].dz - g['dz'])) < 1e-4
+    assert _rel(S['data'].z_est, g['data_z_est']) < 1e-6
+    np.testing.assert_array_equal(S['valid_data'], g['valid_data'])
+    assert _rel(m['dzdt_lag1'].dzdt_lag1, g['m_dzdt_lag1']) < 1e-6
+    np.testing.assert_array_equal(np.isnan(m['z0'].count), np.isnan(g['z0_count']))
+    assert _rel(m['z0'].misfit_rms, g['z0_misfit_rms']) < 1e-5
+    for k in ('R_data', 'RMS_data', 'R_grad2_z0', 'RMS_d2z_dt2'):
+        if k in g.files:
+            key = k.split('_', 1)[1]
+            store = S['R'] if k.startswith('R_') else S['RMS']
+            assert abs(store[key] - float(g[k])) <= 1e-5 * max(abs(float(g[k])), 1e-12), k
+
+
+def test_outer_editing_loop(gpu_available):
+    g = golden('sys_sf3d_edit.npz')
+    S = LS.smooth_fit(data=golden_points(g), **golden_kwargs(g))
+    tse = S['data'].three_sigma_edit
+    flips = np.sum(tse != g['data_three_sigma_edit'].astype(bool))
+    assert flips <= 2                       # points near |r/σ| = 3 may flip
+    if flips == 0:
+        assert _rel(S['m']['z0'].z0, g['z0']) < 1e-6
+        assert _rel(S['data'].sigma_extra, g['data_sigma_extra']) < 1e-5
+    assert S['timing']['lsq_iters'] > 0
+
+
+def test_notebook_amplitude_kat(gpu_available):
+    k = golden('kat.npz')
+    from lssurf_amd import containers as pc
+    W = {'x': 1.e4, 'y': 200, 't': 2}
+    ctr = {'x': 0., 'y': 0., 't': 0.}
+    E_RMS = {'d2z0_dx2': 0.06, 'dz0_dx': 0.06 * 2500, 'd3z_dx2dt': 0.0001, 'd2z_dxdt': 0.0001 * 2500, 'd2z_dt2': 5000}
+    D = {f[3:]: k[f] for f in k.files if f.startswith('in_')}
+    for E, A_ref, A_exp in zip(k['E'], k['A_ref'], k['A_expected']):
+        E_RMS['d2z0_dx2'] = float(E)
+        S = LS.smooth_fit(data=pc.data().from_dict(D), ctr=ctr, W=W, spacing={'z0': 50, 'dz': 100, 'dt': 0.25},
+                          E_RMS=dict(E_RMS), reference_epoch=2, max_iterations=1, VERBOSE=False, dzdt_lags=[1])
+        z0 = S['m']['z0']
+        row = int(z0.z0.shape[0] / 2)
+        A = np.max(np.abs(z0.z0[row, np.abs(z0.x) < 3000]))
+        assert abs(A - A_ref) / A_ref < 1e-6
+        assert abs(A - A_exp) / A_exp < 0.12
