@@ -43,7 +43,8 @@ typedef struct lsq_handle lsq_handle;
  * rules with atol = btol = 1e-10, conlim = 1e8, maxit = 4*n. */
 typedef struct lsq_opts {
     int32_t method;        /* 0 = LSQR (Paige & Saunders 1982)                                 */
-    int32_t precond;       /* 0 = none, 1 = column (Jacobi) scaling                            */
+    int32_t precond;       /* 0 = none, 1 = column (Jacobi) scaling, 2 = dense Cholesky R⁻¹   */
+                           /*     (exact right preconditioner; n up to a few 10^4)             */
     double  atol, btol, conlim;
     int64_t maxit;
     int32_t use_x0;        /* 1: x_inout holds a warm start (outer-iteration "resume")          */
@@ -106,6 +107,13 @@ int lsq_spmv(lsq_handle* h, int32_t trans, const double* x, double* y);
  * stop), starting from the state left by the previous call (first call initialises from b).
  * Times only the device iterations. */
 int lsq_iterate(lsq_handle* h, const double* b, int64_t iters, const lsq_opts* o, lsq_stats* s);
+
+/* ---- error propagation (replaces sparseqr.rz + inv_tr_upper + row RSS, smooth_fit.py:212-253)
+ * Dense device Cholesky AᵀA = RᵀR of the current weighted, masked A (n up to a few 10^4):
+ * lsq_sigma_x: E_j = sqrt(diag((AᵀA)^-1))_j = sqrt(row sums of R^-1 squared), length n;
+ * lsq_get_rinv: R^-1 as a dense n x n row-major upper-triangular matrix. */
+int lsq_sigma_x(lsq_handle* h, double* E);
+int lsq_get_rinv(lsq_handle* h, double* Rinv);
 
 /* Bench / profiling hooks.  lsq_profile_kernels times each iteration kernel in isolation
  * (reps launches each, HIP events on the handle's stream): ms4 = {x/w+SpMV, SpMTV, beta reduce,

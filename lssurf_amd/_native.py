@@ -33,7 +33,8 @@ class LsqStats(ctypes.Structure):
 # every symbol declared in include/lsqsurf.h
 EXPORTS = ['lsq_default_opts', 'lsq_create', 'lsq_destroy', 'lsq_last_error', 'lsq_set_col_map',
            'lsq_set_matrix_coo', 'lsq_set_row_weight', 'lsq_set_row_mask', 'lsq_shape', 'lsq_get_csr',
-           'lsq_solve', 'lsq_spmv', 'lsq_iterate', 'lsq_profile_kernels', 'lsq_sell_info',
+           'lsq_solve', 'lsq_spmv', 'lsq_iterate', 'lsq_profile_kernels', 'lsq_sell_info', 'lsq_sigma_x',
+           'lsq_get_rinv',
            'tri_upper_solve_csr', 'tri_upper_inv_csr', 'tri_upper_rowrss_csr', 'tri_last_error']
 
 _lib = None
@@ -64,6 +65,8 @@ def load():
         'lsq_iterate': ([P, P, i64, P, P], ctypes.c_int),
         'lsq_profile_kernels': ([P, i32, P], ctypes.c_int),
         'lsq_sell_info': ([P, P], ctypes.c_int),
+        'lsq_sigma_x': ([P, P], ctypes.c_int),
+        'lsq_get_rinv': ([P, P], ctypes.c_int),
         'tri_upper_solve_csr': ([i32, i64, P, P, P, P, P], ctypes.c_int),
         'tri_upper_inv_csr': ([i32, i64, P, P, P, i64, ctypes.c_float, P, P, P, P], ctypes.c_int),
         'tri_upper_rowrss_csr': ([i32, i64, P, P, P, P], ctypes.c_int),

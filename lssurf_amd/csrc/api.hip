@@ -11,6 +11,8 @@ void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts&
 int lsqr_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq_stats* stats);
 int lsqr_iterate(System& S, const double* h_b, int64_t iters, const lsq_opts& o, lsq_stats* stats);
 void lsqr_profile(System& S, int reps, double* ms_out);
+void lsqr_sigma_x(System& S, double* h_E);
+void lsqr_get_rinv(System& S, double* h_Ri);
 void graph_cache_drop(const System* S);
 }  // namespace lsq
 
@@ -212,7 +214,7 @@ int lsq_solve(lsq_handle* h, const double* b, double* x_inout, const lsq_opts* o
         lsq_default_opts(&d);
         if (!o) o = &d;
         if (o->method != 0) return fail(S, "lsq_solve: only method 0 (LSQR) is implemented");
-        if (o->precond < 0 || o->precond > 1) return fail(S, "lsq_solve: precond must be 0 or 1");
+        if (o->precond < 0 || o->precond > 2) return fail(S, "lsq_solve: precond must be 0, 1 or 2");
         return lsq::lsqr_solve(S, b, x_inout, *o, s);
     });
 }
@@ -244,6 +246,24 @@ int lsq_sell_info(lsq_handle* h, int64_t* out6) {
         out6[4] = S.AT.nent;
         out6[5] = (int64_t)(S.G.rp.bytes() + S.G.ci.bytes() + S.G.val.bytes() + S.GT.rp.bytes() + S.GT.ci.bytes() +
                             S.GT.val.bytes() + S.A.ci.bytes() + S.A.val.bytes() + S.AT.ci.bytes() + S.AT.val.bytes());
+        return 0;
+    });
+}
+
+int lsq_sigma_x(lsq_handle* h, double* E) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_sigma_x: no matrix");
+        if (!E) return fail(S, "lsq_sigma_x: null output");
+        lsq::lsqr_sigma_x(S, E);
+        return 0;
+    });
+}
+
+int lsq_get_rinv(lsq_handle* h, double* Rinv) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_get_rinv: no matrix");
+        if (!Rinv) return fail(S, "lsq_get_rinv: null output");
+        lsq::lsqr_get_rinv(S, Rinv);
         return 0;
     });
 }

@@ -395,6 +395,7 @@ void refresh_scaling(System& S, int precond) {
     if (!S.rs_dirty && S.cs_mode == precond) return;
     hipLaunchKernelGGL(k_rowscale, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, S.roww.p, S.rowkeep.p, S.rs.p);
     KERNEL_CHECK();
+    S.dense_valid = false;   // the dense factor depends on the row scaling
     if (precond == 1) {
         hipLaunchKernelGGL(k_colnorm, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, S.GT.rp.p, S.GT.ci.p, S.GT.val.p,
                            S.rs.p, S.cs.p);

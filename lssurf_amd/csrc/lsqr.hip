@@ -85,7 +85,8 @@ __global__ __launch_bounds__(BLOCK) void k_init_u(int64_t m, int64_t nslices, co
 // ---- merged: x/w update (blocks [0,gX)) ‖ SpMV u-update (blocks [gX, gX+gA)) ----------------
 __global__ __launch_bounds__(BLOCK) void k_xw_spmv(const LsqState* __restrict__ st, int gX,
                                                    int64_t n, double* __restrict__ y, double* __restrict__ w,
-                                                   const double* __restrict__ vt, int64_t m, int64_t nslices,
+                                                   const double* __restrict__ vt, const double* __restrict__ xs,
+                                                   int xs_scaled, int64_t m, int64_t nslices,
                                                    const int64_t* __restrict__ sp, const int32_t* __restrict__ ci,
                                                    const double* __restrict__ val, double* __restrict__ u,
                                                    double* part_u, double* part_w) {
@@ -106,14 +107,15 @@ __global__ __launch_bounds__(BLOCK) void k_xw_spmv(const LsqState* __restrict__ 
     }
     if (st->stop) return;
     const int bid = blockIdx.x - gX, gA = gridDim.x - gX;
-    const double ia = st->inv_alpha, alpha = st->alpha, ib = st->inv_beta;
+    const double alpha = st->alpha, ib = st->inv_beta;
+    const double ia = xs_scaled ? st->inv_alpha : 1.0;   // precond 2 gathers z = R⁻¹ ṽ/α
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     double su = 0.0;
     for (int64_t s = (int64_t)bid * 4 + wid; s < nslices; s += (int64_t)gA * 4) {
         const int64_t row = s * SELL_C + lane;
         if (row < m) {
             const int64_t base = sp[s];
-            const double ax = sell_row_dot(ci, val, base, (sp[s + 1] - base) / SELL_C, lane, vt);
+            const double ax = sell_row_dot(ci, val, base, (sp[s + 1] - base) / SELL_C, lane, xs);
             const double un = ax * ia - alpha * (u[row] * ib);
             u[row] = un;
             su += un * un;
@@ -127,7 +129,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmtv(const LsqState* __restrict__ st
                                                  const int64_t* __restrict__ sp, const int32_t* __restrict__ ci,
                                                  const double* __restrict__ val, const double* __restrict__ u,
                                                  const double* __restrict__ vin, double* __restrict__ vout,
-                                                 double* part_v) {
+                                                 double* part_v, int raw) {
     if (st->stop) return;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const double ib = st->inv_beta, beta = st->beta, ia = st->inv_alpha;
@@ -136,12 +138,12 @@ __global__ __launch_bounds__(BLOCK) void k_spmtv(const LsqState* __restrict__ st
     for (int64_t s = (int64_t)blockIdx.x * 4 + wid; s < nslices; s += (int64_t)gridDim.x * 4) {
         const int64_t row = s * SELL_C + lane;
         double vn;
-        if (skip) {
+        if (skip && !raw) {
             vn = row < n ? vin[row] : 0.0;
         } else if (row < n) {
             const int64_t base = sp[s];
             const double atu = sell_row_dot(ci, val, base, (sp[s + 1] - base) / SELL_C, lane, u);
-            vn = atu * ib - beta * (vin[row] * ia);
+            vn = raw ? atu : atu * ib - beta * (vin[row] * ia);   // raw: t = Aᵀũ for the R⁻ᵀ epilogue
         } else {
             vn = 0.0;
         }
@@ -312,7 +314,7 @@ __global__ __launch_bounds__(BLOCK) void k_scale(int64_t n, const double* __rest
 }
 
 struct Grids {
-    int gA, gT, gX;
+    int gA, gT, gX, gR, gRT;
 };
 
 Grids grids_for(const System& S) {
@@ -320,18 +322,24 @@ Grids grids_for(const System& S) {
     g.gA = (int)std::min<int64_t>(std::max<int64_t>((S.A.nslices + 3) / 4, 1), NPART);
     g.gT = (int)std::min<int64_t>(std::max<int64_t>((S.AT.nslices + 3) / 4, 1), NPART);
     g.gX = grid_for(S.G.n, BLOCK * 4, NPART);
+    g.gR = grid_for(S.G.n, 4, NPART);        // k_gemv_upper: one wave per row
+    g.gRT = grid_for(S.G.n, BLOCK, NPART);   // k_gemvT_upper: one thread per column
     return g;
 }
 
 void ensure_workspace(System& S) {
     const int64_t m = S.G.m, n = std::max<int64_t>(S.G.n, 1);
-    if (S.u.n != m) S.u.alloc(std::max<int64_t>(m, 1));
-    if (S.bw.n != m) S.bw.alloc(std::max<int64_t>(m, 1));
+    if (S.u.n != std::max<int64_t>(m, 1)) {
+        S.u.alloc(std::max<int64_t>(m, 1));
+        S.bw.alloc(std::max<int64_t>(m, 1));
+    }
     if (S.vb0.n != n) {
         S.vb0.alloc(n);
         S.vb1.alloc(n);
         S.w.alloc(n);
         S.y.alloc(n);
+        S.zt.alloc(n);
+        S.tt.alloc(n);
     }
     if (!S.part_u.p) {
         S.part_u.alloc(NPART);
@@ -343,34 +351,64 @@ void ensure_workspace(System& S) {
 }
 
 // launch one LSQR iteration; parity p: ṽ read from vb[p], written to vb[1-p]
-void launch_iteration(System& S, const Grids& g, int p) {
+void launch_iteration(System& S, const Grids& g, int p, int precond) {
     hipStream_t st = S.stream;
     double* vt = p ? S.vb1.p : S.vb0.p;
     double* vo = p ? S.vb0.p : S.vb1.p;
-    hipLaunchKernelGGL(k_xw_spmv, dim3(g.gX + g.gA), dim3(BLOCK), 0, st, S.st.p, g.gX, S.G.n, S.y.p, S.w.p, vt, S.G.m,
-                       S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p, S.u.p, S.part_u.p, S.part_w.p);
+    const bool dense = precond == 2;
+    if (dense)   // z = R⁻¹ ṽ / α
+        hipLaunchKernelGGL(k_gemv_upper, dim3(g.gR), dim3(BLOCK), 0, st, S.dRi.p, S.G.n, S.dense_ld, vt, S.st.p, 1,
+                           S.zt.p);
+    hipLaunchKernelGGL(k_xw_spmv, dim3(g.gX + g.gA), dim3(BLOCK), 0, st, S.st.p, g.gX, S.G.n, S.y.p, S.w.p, vt,
+                       dense ? S.zt.p : vt, dense ? 0 : 1, S.G.m, S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p, S.u.p,
+                       S.part_u.p, S.part_w.p);
     hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gA, S.part_b.p, 0, 0);
-    hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, S.G.n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
-                       S.AT.val.p, S.u.p, vt, vo, S.part_v.p);
-    hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gT, S.part_w.p, g.gX, 0);
+    if (dense) {
+        hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, S.G.n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
+                           S.AT.val.p, S.u.p, vt, S.tt.p, S.part_v.p, 1);
+        hipLaunchKernelGGL(k_gemvT_upper, dim3(g.gRT), dim3(BLOCK), 0, st, S.dRi.p, S.G.n, S.dense_ld, S.tt.p, S.st.p,
+                           1, vt, vo, S.part_v.p);
+        hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gRT, S.part_w.p, g.gX, 0);
+    } else {
+        hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, S.G.n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
+                           S.AT.val.p, S.u.p, vt, vo, S.part_v.p, 0);
+        hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gT, S.part_w.p, g.gX, 0);
+    }
+}
+
+// final x/w update of a solve that stopped on the last iteration of a batch (newest ṽ in vb0)
+void launch_flush(System& S, const Grids& g) {
+    hipLaunchKernelGGL(k_xw_spmv, dim3(g.gX + g.gA), dim3(BLOCK), 0, S.stream, S.st.p, g.gX, S.G.n, S.y.p, S.w.p,
+                       S.vb0.p, S.vb0.p, 1, S.G.m, S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p, S.u.p, S.part_u.p,
+                       S.part_w.p);
+    hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, S.stream, S.st.p, S.part_u.p, g.gA, S.part_b.p, 0, 0);
+    KERNEL_CHECK();
 }
 
 }  // namespace
 
 // Initialise the LSQR state from rhs b (host, length m, unweighted) and optional warm start
-// x0 (host, length n, or nullptr).  Mirrors scipy lsqr's set-up block.
+// x0 (host, length n, or nullptr).  Mirrors scipy lsqr's set-up block for the operator A·M
+// (M = diag(cs) for precond 0/1, M = R⁻¹ for precond 2).
 void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts& o, bool no_stop) {
     hipStream_t st = S.stream;
     ensure_workspace(S);
     const Grids g = grids_for(S);
     const int64_t m = S.G.m, n = S.G.n;
+    const bool dense = o.precond == 2;
     DBuf<double> db(std::max<int64_t>(m, 1));
     db.upload(h_b, m, st);
-    DBuf<double> dy0;
+    DBuf<double> dx0, dy0;
     if (h_x0) {
+        dx0.alloc(std::max<int64_t>(n, 1));
         dy0.alloc(std::max<int64_t>(n, 1));
-        dy0.upload(h_x0, n, st);
-        hipLaunchKernelGGL(k_scale, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, dy0.p, S.cs.p, 1, dy0.p);
+        dx0.upload(h_x0, n, st);
+        if (dense) {   // y0 = R x0 ; the SELL values are unscaled, so A·M·y0 = A x0
+            hipLaunchKernelGGL(k_gemv_upper, dim3(g.gR), dim3(BLOCK), 0, st, S.dR.p, n, S.dense_ld, dx0.p, nullptr, 2,
+                               dy0.p);
+        } else {       // y0 = x0 / cs ; A·D·y0 = A x0 with the scaled SELL values
+            hipLaunchKernelGGL(k_scale, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, dx0.p, S.cs.p, 1, dy0.p);
+        }
         KERNEL_CHECK();
     }
     LsqState h{};
@@ -381,21 +419,32 @@ void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts&
     h.no_stop = no_stop ? 1 : 0;
     h.cs2 = -1.0;
     HIP_CHECK(hipMemcpyAsync(S.st.p, &h, sizeof(h), hipMemcpyHostToDevice, st));
+    // the SpMV of the warm start gathers in A·M coordinates: y0 for precond 0/1, x0 for precond 2
+    const double* gather0 = h_x0 ? (dense ? dx0.p : dy0.p) : nullptr;
     hipLaunchKernelGGL(k_init_u, dim3(g.gA), dim3(BLOCK), 0, st, m, S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p,
-                       S.rs.p, db.p, dy0.p, S.u.p, S.bw.p, S.part_u.p, S.part_b.p);
+                       S.rs.p, db.p, gather0, S.u.p, S.bw.p, S.part_u.p, S.part_b.p);
     KERNEL_CHECK();
     hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gA, S.part_b.p, g.gA, 1);
     KERNEL_CHECK();
     S.vb1.zero(st);
-    hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
-                       S.AT.val.p, S.u.p, S.vb1.p, S.vb0.p, S.part_v.p);
+    int nv = g.gT;
+    if (dense) {
+        hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
+                           S.AT.val.p, S.u.p, S.vb1.p, S.tt.p, S.part_v.p, 1);
+        hipLaunchKernelGGL(k_gemvT_upper, dim3(g.gRT), dim3(BLOCK), 0, st, S.dRi.p, n, S.dense_ld, S.tt.p, S.st.p, 1,
+                           S.vb1.p, S.vb0.p, S.part_v.p);
+        nv = g.gRT;
+    } else {
+        hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
+                           S.AT.val.p, S.u.p, S.vb1.p, S.vb0.p, S.part_v.p, 0);
+    }
     KERNEL_CHECK();
-    hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gT, S.part_w.p, g.gX, 1);
+    hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, nv, S.part_w.p, g.gX, 1);
     KERNEL_CHECK();
-    hipLaunchKernelGGL(k_init_w, dim3(g.gX), dim3(BLOCK), 0, st, S.st.p, n, S.vb0.p, dy0.p, S.w.p, S.y.p,
-                       S.part_w.p);
+    hipLaunchKernelGGL(k_init_w, dim3(g.gX), dim3(BLOCK), 0, st, S.st.p, n, S.vb0.p, h_x0 ? dy0.p : nullptr, S.w.p,
+                       S.y.p, S.part_w.p);
     KERNEL_CHECK();
-    HIP_CHECK(hipStreamSynchronize(st));   // db / dy0 are released on return
+    HIP_CHECK(hipStreamSynchronize(st));   // db / dx0 / dy0 are released on return
     S.iter_parity = 0;
 }
 
@@ -405,33 +454,36 @@ struct GraphCache {
     const System* sys = nullptr;
     const void* key = nullptr;   // S.u.p identifies the workspace generation
     int batch = 0;
+    int precond = -1;
     hipGraphExec_t exec = nullptr;
 };
 thread_local GraphCache g_cache;
 
 // run `count` iterations starting at parity S.iter_parity (count even when graphs are used)
-void run_batch(System& S, int count, bool use_graph) {
+void run_batch(System& S, int count, bool use_graph, int precond) {
     const Grids g = grids_for(S);
     if (use_graph && count % 2 == 0 && S.iter_parity == 0) {
         GraphCache& c = g_cache;
-        if (c.exec == nullptr || c.sys != &S || c.key != (const void*)S.u.p || c.batch != count) {
+        if (c.exec == nullptr || c.sys != &S || c.key != (const void*)S.u.p || c.batch != count ||
+            c.precond != precond) {
             if (c.exec) (void)hipGraphExecDestroy(c.exec);
             c.exec = nullptr;
             hipGraph_t graph;
             HIP_CHECK(hipStreamBeginCapture(S.stream, hipStreamCaptureModeThreadLocal));
-            for (int i = 0; i < count; ++i) launch_iteration(S, g, i & 1);
+            for (int i = 0; i < count; ++i) launch_iteration(S, g, i & 1, precond);
             HIP_CHECK(hipStreamEndCapture(S.stream, &graph));
             HIP_CHECK(hipGraphInstantiate(&c.exec, graph, nullptr, nullptr, 0));
             HIP_CHECK(hipGraphDestroy(graph));
             c.sys = &S;
             c.key = S.u.p;
             c.batch = count;
+            c.precond = precond;
         }
         HIP_CHECK(hipGraphLaunch(c.exec, S.stream));
         return;
     }
     for (int i = 0; i < count; ++i) {
-        launch_iteration(S, g, S.iter_parity);
+        launch_iteration(S, g, S.iter_parity, precond);
         S.iter_parity ^= 1;
     }
     KERNEL_CHECK();
@@ -453,6 +505,11 @@ void fill_stats(const LsqState& h, lsq_stats* s) {
     s->xnorm = h.xnorm;
 }
 
+void prepare(System& S, int precond) {
+    refresh_scaling(S, precond);
+    if (precond == 2 && !S.dense_valid) dense_factor(S);
+}
+
 }  // namespace
 
 void graph_cache_drop(const System* S) {
@@ -463,7 +520,7 @@ void graph_cache_drop(const System* S) {
 }
 
 int lsqr_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq_stats* stats) {
-    refresh_scaling(S, o.precond);
+    prepare(S, o.precond);
     lsqr_init(S, h_b, o.use_x0 ? h_x : nullptr, o, false);
     int batch = o.batch > 0 ? o.batch : 16;
     batch += batch & 1;
@@ -475,23 +532,22 @@ int lsqr_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq
     HIP_CHECK(hipMemcpyAsync(&h, S.st.p, sizeof(h), hipMemcpyDeviceToHost, S.stream));
     HIP_CHECK(hipStreamSynchronize(S.stream));
     while (!h.stop) {
-        run_batch(S, batch, o.use_graph != 0);
+        run_batch(S, batch, o.use_graph != 0, o.precond);
         HIP_CHECK(hipMemcpyAsync(&h, S.st.p, sizeof(h), hipMemcpyDeviceToHost, S.stream));
         HIP_CHECK(hipStreamSynchronize(S.stream));
     }
-    if (!h.finished) {   // apply the final x/w update
+    const Grids g = grids_for(S);
+    if (!h.finished) {   // stop on the last iteration of a batch: apply its x/w update
         S.iter_parity = 0;
-        const Grids g = grids_for(S);
-        // after an even batch the newest ṽ is in vb0; the flush only needs the x/w part
-        hipLaunchKernelGGL(k_xw_spmv, dim3(g.gX + g.gA), dim3(BLOCK), 0, S.stream, S.st.p, g.gX, S.G.n, S.y.p, S.w.p,
-                           S.vb0.p, S.G.m, S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p, S.u.p, S.part_u.p,
-                           S.part_w.p);
-        hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, S.stream, S.st.p, S.part_u.p, g.gA, S.part_b.p, 0, 0);
-        KERNEL_CHECK();
+        launch_flush(S, g);
     }
     HIP_CHECK(hipEventRecord(e1, S.stream));
     const int64_t n = S.G.n;
-    hipLaunchKernelGGL(k_scale, dim3(grid_for(n)), dim3(BLOCK), 0, S.stream, n, S.y.p, S.cs.p, 0, S.vb1.p);
+    if (o.precond == 2)
+        hipLaunchKernelGGL(k_gemv_upper, dim3(g.gR), dim3(BLOCK), 0, S.stream, S.dRi.p, n, S.dense_ld, S.y.p, nullptr,
+                           2, S.vb1.p);
+    else
+        hipLaunchKernelGGL(k_scale, dim3(grid_for(n)), dim3(BLOCK), 0, S.stream, n, S.y.p, S.cs.p, 0, S.vb1.p);
     KERNEL_CHECK();
     S.vb1.download(h_x, n, S.stream);
     HIP_CHECK(hipMemcpyAsync(&h, S.st.p, sizeof(h), hipMemcpyDeviceToHost, S.stream));
@@ -510,7 +566,7 @@ int lsqr_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq
 }
 
 int lsqr_iterate(System& S, const double* h_b, int64_t iters, const lsq_opts& o, lsq_stats* stats) {
-    refresh_scaling(S, o.precond);
+    prepare(S, o.precond);
     if (!S.iter_ready) {
         lsq_opts oo = o;
         oo.maxit = INT64_MAX / 4;
@@ -526,7 +582,7 @@ int lsqr_iterate(System& S, const double* h_b, int64_t iters, const lsq_opts& o,
     int64_t left = iters;
     while (left > 0) {
         const int c = (int)std::min<int64_t>(left, batch);
-        run_batch(S, c, o.use_graph != 0 && c == batch);
+        run_batch(S, c, o.use_graph != 0 && c == batch, o.precond);
         left -= c;
     }
     HIP_CHECK(hipEventRecord(e1, S.stream));
@@ -563,11 +619,11 @@ void lsqr_profile(System& S, int reps, double* ms_out /* [4]: xw_spmv, spmtv, be
             for (int r = 0; r < reps; ++r) {
                 if (k == 0)
                     hipLaunchKernelGGL(k_xw_spmv, dim3(g.gX + g.gA), dim3(BLOCK), 0, S.stream, S.st.p, g.gX, S.G.n,
-                                       S.y.p, S.w.p, S.vb0.p, S.G.m, S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p,
-                                       S.u.p, S.part_u.p, S.part_w.p);
+                                       S.y.p, S.w.p, S.vb0.p, S.vb0.p, 1, S.G.m, S.A.nslices, S.A.sp.p, S.A.ci.p,
+                                       S.A.val.p, S.u.p, S.part_u.p, S.part_w.p);
                 else if (k == 1)
                     hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, S.stream, S.st.p, S.G.n, S.AT.nslices,
-                                       S.AT.sp.p, S.AT.ci.p, S.AT.val.p, S.u.p, S.vb0.p, S.vb1.p, S.part_v.p);
+                                       S.AT.sp.p, S.AT.ci.p, S.AT.val.p, S.u.p, S.vb0.p, S.vb1.p, S.part_v.p, 0);
                 else if (k == 2)
                     hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, S.stream, S.st.p, S.part_u.p, g.gA,
                                        S.part_b.p, 0, 2);
@@ -585,6 +641,26 @@ void lsqr_profile(System& S, int reps, double* ms_out /* [4]: xw_spmv, spmtv, be
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     S.iter_ready = false;
+}
+
+// sqrt(diag((AᵀA)⁻¹)) for the current row weights / mask, via the dense factor.
+void lsqr_sigma_x(System& S, double* h_E) {
+    refresh_scaling(S, S.cs_mode < 0 ? 0 : S.cs_mode);
+    if (!S.dense_valid) dense_factor(S);
+    DBuf<double> dE(std::max<int64_t>(S.G.n, 1));
+    dense_rowrss(S, dE.p);
+    dE.download(h_E, S.G.n, S.stream);
+    HIP_CHECK(hipStreamSynchronize(S.stream));
+}
+
+// Download R⁻¹ (n x n, row-major, upper triangular) of the dense factor.
+void lsqr_get_rinv(System& S, double* h_Ri) {
+    refresh_scaling(S, S.cs_mode < 0 ? 0 : S.cs_mode);
+    if (!S.dense_valid) dense_factor(S);
+    const int64_t n = S.G.n, ld = S.dense_ld;
+    HIP_CHECK(hipMemcpy2DAsync(h_Ri, n * sizeof(double), S.dRi.p, ld * sizeof(double), n * sizeof(double), n,
+                               hipMemcpyDeviceToHost, S.stream));
+    HIP_CHECK(hipStreamSynchronize(S.stream));
 }
 
 }  // namespace lsq

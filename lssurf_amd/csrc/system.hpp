@@ -67,8 +67,13 @@ struct System {
     bool rs_dirty = true;
     Sell A, AT;
 
+    // dense factor (precond 2 / error propagation): R and R⁻¹, npad x npad row-major
+    DBuf<double> dR, dRi;
+    int64_t dense_ld = 0;
+    bool dense_valid = false;
+
     // LSQR workspace
-    DBuf<double> u, vb0, vb1, w, y, bw;
+    DBuf<double> u, vb0, vb1, w, y, bw, zt, tt;
     DBuf<double> part_u, part_v, part_w, part_b;
     DBuf<LsqState> st;
     bool iter_ready = false;   // lsq_iterate state initialised
@@ -82,5 +87,13 @@ void form_from_coo(System& S, int64_t m, int64_t n_full, int64_t nnz, const int6
                    const int64_t* c, const double* v);
 void refresh_scaling(System& S, int precond);   // rs/cs -> SELL values
 void csr_spmv(System& S, int trans, const double* dx, double* dy);  // unweighted G / Gᵀ products
+
+// dense.hip
+void dense_factor(System& S);                     // R, R⁻¹ of diag(rs)·G (throws if not SPD)
+void dense_rowrss(System& S, double* dE);         // sqrt(row sums of R⁻¹²) = sqrt(diag((AᵀA)⁻¹))
+__global__ void k_gemv_upper(const double* M, int64_t n, int64_t ld, const double* v, const LsqState* st,
+                             int scale_mode, double* z);
+__global__ void k_gemvT_upper(const double* M, int64_t n, int64_t ld, const double* t, const LsqState* st, int mode,
+                              const double* vin, double* out, double* part);
 
 }  // namespace lsq

@@ -46,7 +46,7 @@ DEFAULTS = {'reference_epoch': 0, 'W_ctr': 1e4, 'return_fit_objects': False, 'ma
             # lssurf_amd solver options (new keys; defaults reproduce the exact LS solution to
             # the tolerance documented in DESIGN.md §Parity)
             'device': 0, 'lsq_atol': 1e-12, 'lsq_btol': 1e-12, 'lsq_conlim': 1e12, 'lsq_maxit': 0,
-            'lsq_precond': 1, 'lsq_warm_start': True}
+            'lsq_precond': 'auto', 'lsq_dense_max': 16384, 'lsq_warm_start': True}
 
 OUT_OF_SCOPE = ('bias_params', 'sensor_grid_bias_params', 'prior_args', 'prior_edge_args', 'lagrangian_coords',
                 'constraint_scaling_maps', 'mask_file', 'avg_masks', 'z0_average_scale', 'bias_edit_vals')
@@ -104,9 +104,14 @@ def print_TOC(G_data, Gc):
             print(f'\t{name}: {len(np.unique(rr)) / 1000}K')
 
 
-def _solve_opts(args):
-    return dict(atol=args['lsq_atol'], btol=args['lsq_btol'], conlim=args['lsq_conlim'], maxit=args['lsq_maxit'],
-                precond=args['lsq_precond'])
+def _solve_opts(args, n):
+    """LSQR options.  precond 'auto': the exact dense-Cholesky preconditioner (R⁻¹ on the
+    device) when n <= lsq_dense_max, column scaling otherwise (maxit 50 n for those)."""
+    pc_ = args['lsq_precond']
+    if pc_ == 'auto':
+        pc_ = 2 if n <= args['lsq_dense_max'] else 1
+    maxit = args['lsq_maxit'] or (0 if pc_ == 2 else 50 * n)
+    return dict(atol=args['lsq_atol'], btol=args['lsq_btol'], conlim=args['lsq_conlim'], maxit=maxit, precond=pc_)
 
 
 def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grids, sigma_extra_masks=None):
@@ -132,7 +137,10 @@ def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grid
         tic = time()
         m0_last = m0
         x0 = x if (args['lsq_warm_start'] and x is not None) else None
-        x = system.solve(weight, in_TSE, rhs, x0=x0, **_solve_opts(args))
+        x = system.solve(weight, in_TSE, rhs, x0=x0, **_solve_opts(args, system.keep_cols.size))
+        if system.stats['istop'] == 7:
+            print(f"smooth_fit: LSQR reached its iteration limit ({system.stats['iters']}) before the "
+                  f"requested tolerance; raise lsq_maxit or use lsq_precond=2", flush=True)
         m0 = system.expand(x)
         timing['sparseqr_solve'] = time() - tic
         timing['lsq_iters'] += int(system.stats['iters'])

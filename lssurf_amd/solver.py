@@ -122,6 +122,18 @@ class LSQSolver:
         self._check(self._L.lsq_sell_info(self._h, ptr(o)), 'lsq_sell_info')
         return dict(zip(['m', 'n', 'nnz', 'sell_A', 'sell_AT', 'device_bytes'], o.tolist()))
 
+    def sigma_x(self):
+        """sqrt(diag((AᵀA)⁻¹)) of the current weighted, masked system (dense device Cholesky)."""
+        E = np.zeros(self.n)
+        self._check(self._L.lsq_sigma_x(self._h, ptr(E)), 'lsq_sigma_x')
+        return E
+
+    def rinv(self):
+        """R⁻¹ (n x n upper triangular, AᵀA = RᵀR) of the current weighted, masked system."""
+        Ri = np.zeros((self.n, self.n))
+        self._check(self._L.lsq_get_rinv(self._h, ptr(Ri)), 'lsq_get_rinv')
+        return Ri
+
     def spmv(self, x, trans=False):
         """G x (trans False) or Gᵀ x on the UNWEIGHTED formed operator, all rows."""
         x = as_c(x, np.float64)

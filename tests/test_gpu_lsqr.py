@@ -193,3 +193,44 @@ def test_medium_system_formation_and_solve(gpu_available):
     np.testing.assert_array_equal(A.data, Aref.data)
     xc, stc = cpu.lsqr(Aref, wgt * rhs, atol=1e-12, btol=1e-12, conlim=1e12)
     assert np.linalg.norm(xg - xc) / np.linalg.norm(xc) < 1e-8
+
+
+@pytest.mark.parametrize('name', ['sf3d', 'nb_xt'])
+def test_dense_preconditioned_lsqr(gpu_available, name):
+    """precond 2 (device Cholesky R⁻¹ as right preconditioner): converges in a few iterations."""
+    g, S, sysm, w, rhs = _fit_system(name)
+    x = sysm.solve(w, np.ones(sysm.n_data, bool), rhs, atol=1e-14, btol=1e-14, conlim=1e16, precond=2)
+    st = sysm.stats
+    E = sysm.solver.sigma_x()
+    Ri = sysm.solver.rinv()
+    sysm.close()
+    assert st['iters'] < 60, st
+    assert np.linalg.norm(x - g['x']) / np.linalg.norm(g['x']) < 1e-10
+    A = golden_csr(g)
+    np.testing.assert_allclose(E, dense.diag_inv_normal(A), rtol=1e-8)
+    R = np.linalg.inv(Ri)
+    N = (A.T @ A).toarray()
+    assert np.linalg.norm(R.T @ R - N) / np.linalg.norm(N) < 1e-12
+    assert np.allclose(np.tril(Ri, -1), 0)
+
+
+def test_dense_precond_stiff_kat_system(gpu_available):
+    """The stiff notebook case (E_d2z0_dx2 = 0.0003, cond ~1e7) that column-scaled LSQR needs
+    ~47 k iterations for."""
+    from lssurf_amd import containers as pc
+    k = golden('kat.npz')
+    D = pc.data().from_dict({f[3:]: k[f] for f in k.files if f.startswith('in_')})
+    E_RMS = {'d2z0_dx2': 0.0003, 'dz0_dx': 150., 'd3z_dx2dt': 0.0001, 'd2z_dxdt': 0.25, 'd2z_dt2': 5000}
+    S = LS.smooth_fit(data=D, ctr={'x': 0., 'y': 0., 't': 0.}, W={'x': 1.e4, 'y': 200, 't': 2},
+                      spacing={'z0': 50, 'dz': 100, 'dt': 0.25}, E_RMS=E_RMS, reference_epoch=2, VERBOSE=False,
+                      return_fit_objects=True)
+    keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], 2)
+    fs = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N)
+    w = 1. / np.sqrt((1 / (1. / np.concatenate((S['Ed'], S['Ec'])))) ** 2)
+    rhs = np.zeros(w.size)
+    rhs[:S['data'].size] = S['data'].z
+    x = fs.solve(w, np.ones(fs.n_data, bool), rhs, atol=1e-14, btol=1e-14, conlim=1e16, precond=2)
+    A = fs.solver.get_csr()
+    fs.close()
+    xs = dense.ls_solve_dense(A, w * rhs)
+    assert np.linalg.norm(x - xs) / np.linalg.norm(xs) < 1e-9

@@ -63,3 +63,14 @@ def test_notebook_amplitude_kat(gpu_available):
         A = np.max(np.abs(z0.z0[row, np.abs(z0.x) < 3000]))
         assert abs(A - A_ref) / A_ref < 1e-6
         assert abs(A - A_exp) / A_exp < 0.12
+
+
+def test_compute_E_matches_reference(gpu_available):
+    """smooth_fit(compute_E=True): sigma_z0 / sigma_dz / sigma_dzdt_lag1 vs the reference's
+    rz + inv_tr_upper path (notebook cell 45 configuration)."""
+    g = golden('sys_nb_err.npz')
+    S = LS.smooth_fit(data=golden_points(g), **golden_kwargs(g))
+    E = S['E']
+    assert _rel(E['sigma_z0'].sigma_z0, g['E_sigma_z0']) < 1e-7
+    assert _rel(E['sigma_dz'].sigma_dz, g['E_sigma_dz']) < 1e-7
+    assert _rel(E['sigma_dzdt_lag1'].sigma_dzdt_lag1, g['E_sigma_dzdt_lag1']) < 1e-6
