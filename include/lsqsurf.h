@@ -84,6 +84,35 @@ int lsq_set_matrix_coo(lsq_handle* h, int64_t m, int64_t n_full, int64_t nnz,
                        const int64_t* r, const int64_t* c, const double* v,
                        const double* row_weight);
 
+/* Structured formation (no host triplets): the smooth_fit operator described by its fd_grids
+ * and stencils, rows generated on the device exactly as lin_op would generate them.
+ *   data rows 0..npts-1: sum over `n_interp` interpolation parts (lin_op.interp_mtx,
+ *     lin_op.py:163-247) of point p = (py, px[, pt]) on grid interp_grid[k]; points must be
+ *     inside every grid (bounds_error=True semantics);
+ *   stencil part s covers rows [row0, row0+n_eq): centre k -> subscripts lo + unravel(k, hi-lo)
+ *     ('ij' meshgrid order), entries col0 + ravel(centre + off[t]) with value val[t]
+ *     (lin_op.diff_op, lin_op.py:80-132).
+ * Then the same zero-drop / duplicate-sum / col-map rules as lsq_set_matrix_coo. */
+typedef struct lsq_grid_desc {
+    int32_t ndim, reserved;
+    int64_t shape[3];
+    int64_t col0;
+    double  b0[3], delta[3];
+} lsq_grid_desc;
+typedef struct lsq_stencil_desc {
+    int32_t grid, ntpl;
+    int32_t off[8][3];
+    double  val[8];
+    int64_t row0, n_eq;
+    int64_t lo[3], hi[3];
+} lsq_stencil_desc;
+int lsq_set_matrix_stencil(lsq_handle* h, int64_t m, int64_t n_full,
+                           int32_t n_grids, const lsq_grid_desc* grids,
+                           int32_t n_interp, const int32_t* interp_grid, int64_t npts,
+                           const double* py, const double* px, const double* pt,
+                           int32_t n_stencil, const lsq_stencil_desc* stencils,
+                           const double* row_weight);
+
 /* Replace the row weights (TCinv of iterate_fit, smooth_fit.py:123-129) without re-forming. */
 int lsq_set_row_weight(lsq_handle* h, const double* row_weight);
 /* Row selection Ip_r (smooth_fit.py:132-135): rows with keep[i] == 0 are excluded from the

@@ -20,6 +20,17 @@ class LsqOpts(ctypes.Structure):
                 ('reserved', ctypes.c_int32)]
 
 
+class GridDesc(ctypes.Structure):
+    _fields_ = [('ndim', ctypes.c_int32), ('reserved', ctypes.c_int32), ('shape', ctypes.c_int64 * 3),
+                ('col0', ctypes.c_int64), ('b0', ctypes.c_double * 3), ('delta', ctypes.c_double * 3)]
+
+
+class StencilDesc(ctypes.Structure):
+    _fields_ = [('grid', ctypes.c_int32), ('ntpl', ctypes.c_int32), ('off', (ctypes.c_int32 * 3) * 8),
+                ('val', ctypes.c_double * 8), ('row0', ctypes.c_int64), ('n_eq', ctypes.c_int64),
+                ('lo', ctypes.c_int64 * 3), ('hi', ctypes.c_int64 * 3)]
+
+
 class LsqStats(ctypes.Structure):
     _fields_ = [('iters', ctypes.c_int64), ('istop', ctypes.c_int32), ('reserved', ctypes.c_int32),
                 ('r1norm', ctypes.c_double), ('r2norm', ctypes.c_double), ('anorm', ctypes.c_double),
@@ -32,7 +43,7 @@ class LsqStats(ctypes.Structure):
 
 # every symbol declared in include/lsqsurf.h
 EXPORTS = ['lsq_default_opts', 'lsq_create', 'lsq_destroy', 'lsq_last_error', 'lsq_set_col_map',
-           'lsq_set_matrix_coo', 'lsq_set_row_weight', 'lsq_set_row_mask', 'lsq_shape', 'lsq_get_csr',
+           'lsq_set_matrix_coo', 'lsq_set_matrix_stencil', 'lsq_set_row_weight', 'lsq_set_row_mask', 'lsq_shape', 'lsq_get_csr',
            'lsq_solve', 'lsq_spmv', 'lsq_iterate', 'lsq_profile_kernels', 'lsq_sell_info', 'lsq_sigma_x',
            'lsq_get_rinv',
            'tri_upper_solve_csr', 'tri_upper_inv_csr', 'tri_upper_rowrss_csr', 'tri_last_error']
@@ -57,6 +68,7 @@ def load():
         'lsq_set_col_map': ([P, i64, P, i64], ctypes.c_int),
         'lsq_set_matrix_coo': ([P, i64, i64, i64, P, P, P, P], ctypes.c_int),
         'lsq_set_row_weight': ([P, P], ctypes.c_int),
+        'lsq_set_matrix_stencil': ([P, i64, i64, i32, P, i32, P, i64, P, P, P, i32, P, P], ctypes.c_int),
         'lsq_set_row_mask': ([P, P], ctypes.c_int),
         'lsq_shape': ([P, P, P, P], ctypes.c_int),
         'lsq_get_csr': ([P, P, P, P], ctypes.c_int),

@@ -14,6 +14,9 @@ void lsqr_profile(System& S, int reps, double* ms_out);
 void lsqr_sigma_x(System& S, double* h_E);
 void lsqr_get_rinv(System& S, double* h_Ri);
 void graph_cache_drop(const System* S);
+void form_from_stencils(System& S, int64_t m, int64_t n_full, int32_t n_grids, const lsq_grid_desc* grids,
+                        int32_t n_interp, const int32_t* interp_grid, int64_t npts, const double* py,
+                        const double* px, const double* pt, int32_t n_stencil, const lsq_stencil_desc* st);
 }  // namespace lsq
 
 struct lsq_handle {
@@ -120,6 +123,28 @@ int lsq_set_matrix_coo(lsq_handle* h, int64_t m, int64_t n_full, int64_t nnz, co
         if (S.G.rp.p) return fail(S, "lsq_set_matrix_coo: matrix already set (create a new handle)");
         lsq::graph_cache_drop(&S);
         lsq::form_from_coo(S, m, n_full, nnz, r, c, v);
+        if (row_weight) {
+            S.roww.upload(row_weight, m, S.stream);
+            HIP_CHECK(hipStreamSynchronize(S.stream));
+        }
+        return 0;
+    });
+}
+
+int lsq_set_matrix_stencil(lsq_handle* h, int64_t m, int64_t n_full, int32_t n_grids, const lsq_grid_desc* grids,
+                           int32_t n_interp, const int32_t* interp_grid, int64_t npts, const double* py,
+                           const double* px, const double* pt, int32_t n_stencil, const lsq_stencil_desc* stencils,
+                           const double* row_weight) {
+    return guarded(h, [&](lsq::System& S) {
+        if (m <= 0 || n_full <= 0 || npts < 0 || !grids || (n_interp && !interp_grid) || (n_stencil && !stencils))
+            return fail(S, "lsq_set_matrix_stencil: bad arguments");
+        if (S.have_colmap && n_full != S.n_full) return fail(S, "lsq_set_matrix_stencil: n_full differs from col map");
+        if (m >= (int64_t)INT32_MAX || n_full >= (int64_t)INT32_MAX)
+            return fail(S, "lsq_set_matrix_stencil: dimensions must fit int32 column indices");
+        if (S.G.rp.p) return fail(S, "lsq_set_matrix_stencil: matrix already set (create a new handle)");
+        lsq::graph_cache_drop(&S);
+        lsq::form_from_stencils(S, m, n_full, n_grids, grids, n_interp, interp_grid, npts, py, px, pt, n_stencil,
+                                stencils);
         if (row_weight) {
             S.roww.upload(row_weight, m, S.stream);
             HIP_CHECK(hipStreamSynchronize(S.stream));

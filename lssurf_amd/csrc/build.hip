@@ -348,7 +348,16 @@ void form_from_coo(System& S, int64_t m, int64_t n_full, int64_t nnz, const int6
     tc.release();
     tv.release();
     off.release();
+    finish_formation(S);
+}
 
+// G (canonical CSR, set) -> GT, SELL copies, default scaling state.
+void finish_formation(System& S) {
+    hipStream_t st = S.stream;
+    Csr& G = S.G;
+    const int64_t m = G.m, n = G.n;
+    DBuf<BuildErr> err(1);
+    err.zero(st);
     // transpose
     Csr& T = S.GT;
     T.m = n;

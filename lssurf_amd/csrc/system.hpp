@@ -85,6 +85,7 @@ struct System {
 // build.hip
 void form_from_coo(System& S, int64_t m, int64_t n_full, int64_t nnz, const int64_t* r,
                    const int64_t* c, const double* v);
+void finish_formation(System& S);              // G set -> GT, SELL copies, default scaling
 void refresh_scaling(System& S, int precond);   // rs/cs -> SELL values
 void csr_spmv(System& S, int trans, const double* dx, double* dy);  // unweighted G / Gᵀ products
 

@@ -64,10 +64,11 @@ class lin_op:
         self.N_eq = 0
         self.name = name
         self.id = None
-        self.r = np.array([], dtype=int)
-        self.c = np.array([], dtype=int)
-        self.v = np.array([], dtype=float)
-        self.ind0 = np.zeros([0], dtype=int)
+        self._r = np.array([], dtype=int)
+        self._c = np.array([], dtype=int)
+        self._v = np.array([], dtype=float)
+        self._ind0 = np.zeros([0], dtype=int)
+        self._lazy = None         # callable -> (r, c, v, ind0), evaluated on first access
         self.TOC = {'rows': {}, 'cols': {}}
         self.dst_grid = None
         self.dst_ind0 = None
@@ -80,6 +81,34 @@ class lin_op:
     def __update_size_and_shape__(self):
         self.shape = (self.N_eq, self.col_N)
 
+    # ---- lazy triplets: structure-only operators materialise (r, c, v, ind0) on first use -----
+    def _materialize(self):
+        if self._lazy is not None:
+            f, self._lazy = self._lazy, None
+            self._r, self._c, self._v, self._ind0 = f()
+
+    def _prop(name, structural):
+        def get(self):
+            self._materialize()
+            return getattr(self, '_' + name)
+
+        def put(self, value):
+            self._materialize()
+            setattr(self, '_' + name, value)
+            if structural:
+                self.parts = None      # values changed from outside: structure no longer describes them
+        return property(get, put)
+
+    r = _prop('r', True)
+    c = _prop('c', True)
+    v = _prop('v', True)
+    ind0 = _prop('ind0', False)
+    del _prop
+
+    @property
+    def materialized(self):
+        return self._lazy is None
+
     # ---- helpers ---------------------------------------------------------------------------
     def apply_xform(self, pts, xform=None, dims=(0, 1)):
         if xform is None:
@@ -91,47 +120,68 @@ class lin_op:
         return [T[:, d].ravel() for d in dims]
 
     def ravel(self):
-        self.r, self.c, self.v = np.ravel(self.r), np.ravel(self.c), np.ravel(self.v)
+        if self._lazy is not None:
+            f = self._lazy
+            self._lazy = lambda: tuple(np.ravel(a) for a in f())
+        else:
+            self._r, self._c, self._v = np.ravel(self._r), np.ravel(self._c), np.ravel(self._v)
         return self
 
     def fix_dtypes(self):
-        self.r = self.r.astype(int)
-        self.c = self.c.astype(int)
+        self._materialize()
+        self._r = self._r.astype(int)
+        self._c = self._c.astype(int)
 
     # ---- stencils ----------------------------------------------------------------------------
     def diff_op(self, delta_subs, vals, which_nodes=None, valid_equations_only=True):
         g = self.grid
         nd = min(len(delta_subs), g.N_dims)   # extra offset rows are ignored (zip semantics)
-        lo = [max(0, -int(np.min(ds))) if valid_equations_only else 0 for ds in delta_subs]
+        lo = [max(0, -int(np.min(ds))) if valid_equations_only else 0 for ds in delta_subs[:nd]]
         hi = [min(int(g.shape[k]), int(g.shape[k]) - int(np.max(delta_subs[k])))
               if valid_equations_only else int(g.shape[k]) for k in range(nd)]
-        centres = [s.ravel() for s in np.meshgrid(*[np.arange(a, b) for a, b in zip(lo, hi)], indexing='ij')]
-        if which_nodes is not None:
-            keep = np.isin(g.global_ind(centres), which_nodes)
-            centres = [s[keep] for s in centres]
-        n_eq, n_tpl = centres[0].size, len(delta_subs[0])
-        R = np.empty((n_eq, n_tpl), dtype=int)
-        C = np.empty((n_eq, n_tpl), dtype=int)
-        V = np.empty((n_eq, n_tpl), dtype=float)
-        rows = self.row_0 + np.arange(0, n_eq, dtype=int)
-        for k in range(n_tpl):
-            sub = [centres[d] + delta_subs[d][k] for d in range(nd)]
-            R[:, k] = rows
-            if valid_equations_only:
-                C[:, k] = g.global_ind(sub)
-                V[:, k] = np.ravel(vals[k])
-            else:
-                C[:, k], ok = g.global_ind(sub, return_valid=True)
-                V[:, k] = np.ravel(vals[k]) * np.ravel(ok)
-        self.r, self.c, self.v = R, C, V
+        n_tpl = len(delta_subs[0])
+        row_0 = self.row_0
+
+        def centres_of():
+            cs = [s.ravel() for s in np.meshgrid(*[np.arange(a, b) for a, b in zip(lo, hi)], indexing='ij')]
+            if which_nodes is not None:
+                keep = np.isin(g.global_ind(cs), which_nodes)
+                cs = [s[keep] for s in cs]
+            return cs
+
+        def build():
+            cs = centres_of()
+            n_eq = cs[0].size
+            R = np.empty((n_eq, n_tpl), dtype=int)
+            C = np.empty((n_eq, n_tpl), dtype=int)
+            V = np.empty((n_eq, n_tpl), dtype=float)
+            rows = row_0 + np.arange(0, n_eq, dtype=int)
+            for k in range(n_tpl):
+                sub = [cs[d] + delta_subs[d][k] for d in range(nd)]
+                R[:, k] = rows
+                if valid_equations_only:
+                    C[:, k] = g.global_ind(sub)
+                    V[:, k] = np.ravel(vals[k])
+                else:
+                    C[:, k], ok = g.global_ind(sub, return_valid=True)
+                    V[:, k] = np.ravel(vals[k]) * np.ravel(ok)
+            return R, C, V, g.global_ind(cs).ravel()
+
+        simple = valid_equations_only and which_nodes is None and all(np.size(vv) == 1 for vv in vals)
+        if simple:
+            n_eq = int(np.prod([max(b - a, 0) for a, b in zip(lo, hi)]))
+            self._lazy = build
+            self.parts = [dict(kind='stencil', grid=g, subs=[list(map(int, ds)) for ds in delta_subs[:nd]],
+                               vals=np.array([float(np.ravel(vals[k])[0]) for k in range(n_tpl)]),
+                               lo=lo, hi=hi, row0=0, n_eq=n_eq, row_base=row_0)]
+        else:
+            self._lazy = None
+            self._r, self._c, self._v, self._ind0 = build()
+            n_eq = self._r.shape[0]
+            self.parts = None
         self.N_eq = n_eq
-        self.ind0 = g.global_ind(centres).ravel()
-        self.TOC['rows'] = {self.name: range(self.N_eq)}
+        self.TOC['rows'] = {self.name: np.arange(self.N_eq)}
         self.TOC['cols'] = {g.name: np.arange(g.col_0, g.col_0 + g.N_nodes)}
-        simple = valid_equations_only and which_nodes is None
-        self.parts = [dict(kind='stencil', grid=g, subs=[list(map(int, ds)) for ds in delta_subs[:nd]],
-                           vals=np.array([float(np.ravel(vals[k])[0]) for k in range(n_tpl)]),
-                           row0=0, n_eq=n_eq)] if simple and all(np.size(vv) == 1 for vv in vals) else None
         self.__update_size_and_shape__()
         return self
 
@@ -203,17 +253,19 @@ class lin_op:
         corners = np.c_[[k.ravel() for k in np.mgrid[tuple(slice(0, 2) for _ in range(g.N_dims))]]] \
             if g.N_dims > 1 else np.array([[0, 1]])
         n_nb, npts = corners.shape[1], rows.size
-        R = np.zeros([npts, n_nb], dtype=int)
-        C = np.zeros([npts, n_nb], dtype=int)
-        V = np.ones([npts, n_nb], dtype=float)
-        for k in range(n_nb):
-            R[:, k] = rows
-            C[:, k] = base + np.sum(g.stride * corners[:, k])
-            for d in range(g.N_dims):
-                V[:, k] *= frac[d] if corners[d, k] else (1. - frac[d])
-        self.r, self.c, self.v = R, C, V
+
+        def build():
+            R = np.zeros([npts, n_nb], dtype=int)
+            C = np.zeros([npts, n_nb], dtype=int)
+            V = np.ones([npts, n_nb], dtype=float)
+            for k in range(n_nb):
+                R[:, k] = rows
+                C[:, k] = base + np.sum(g.stride * corners[:, k])
+                for d in range(g.N_dims):
+                    V[:, k] *= frac[d] if corners[d, k] else (1. - frac[d])
+            return R, C, V, np.arange(0, npts, dtype='int')
+        self._lazy = build
         self.N_eq = npts
-        self.ind0 = np.arange(0, npts, dtype='int')
         self.TOC['rows'] = {self.name: np.arange(self.N_eq, dtype='int')}
         self.TOC['cols'] = {g.name: np.arange(g.col_0, g.col_0 + g.N_nodes)}
         self.parts = [dict(kind='interp', grid=g, pts=pts, rows=rows, row0=0, n_eq=npts)] \
@@ -227,10 +279,12 @@ class lin_op:
             for each in op:
                 self.add(each)
             return self
-        self.r = np.append(self.r, op.r)
-        self.c = np.append(self.c, op.c)
-        self.v = np.append(self.v, op.v)
-        self.ind0 = np.append(self.ind0, op.ind0)
+        mine = self._lazy if self._lazy is not None else (lambda a=(self._r, self._c, self._v, self._ind0): a)
+
+        def build(mine=mine, op=op):
+            r, c, v, i0 = mine()
+            return np.append(r, op.r), np.append(c, op.c), np.append(v, op.v), np.append(i0, op.ind0)
+        self._lazy = build
         for key, cols in op.TOC['cols'].items():
             self.TOC['cols'][key] = cols
         self.col_N = np.maximum(self.col_N, op.col_N)
@@ -259,13 +313,11 @@ class lin_op:
         if self.col_N is None:
             self.col_N = np.max(np.array([op.col_N for op in ops]))
         self.TOC['cols'] = TOC_cols
-        rr, cc, vv, ee, parts = [], [], [], [], []
+        ee, parts, offsets = [], [], []
         offset = 0
         for i in order:
             op = ops[i]
-            rr.append(np.ravel(op.r) + offset)
-            cc.append(np.ravel(op.c))
-            vv.append(np.ravel(op.v))
+            offsets.append((op, offset))
             if op.expected is not None:
                 ee.append(np.ravel(op.expected))
             label = op.name if op.name is not None else 'eq'
@@ -286,10 +338,15 @@ class lin_op:
                 parts = None
             offset += op.N_eq
         self.N_eq = offset
-        self.r, self.c, self.v = np.concatenate(rr), np.concatenate(cc), np.concatenate(vv)
+
+        def build(offsets=offsets, ops=tuple(ops)):
+            return (np.concatenate([np.ravel(op.r) + off for op, off in offsets]),
+                    np.concatenate([np.ravel(op.c) for op, _ in offsets]),
+                    np.concatenate([np.ravel(op.v) for op, _ in offsets]),
+                    np.concatenate([op.ind0 for op in ops]))
+        self._lazy = build
         if ee:
             self.expected = np.concatenate(ee)
-        self.ind0 = np.concatenate([op.ind0 for op in ops])
         if self.name is not None and len(self.name) > 0:
             self.TOC['rows'][self.name] = np.arange(0, offset)
         self.parts = parts
@@ -302,6 +359,17 @@ class lin_op:
             mask = self.grid.mask
         if mask is None:
             return np.ones_like(self.ind0, dtype=float)
+        flat = np.ravel(mask)
+        if flat.size and np.all(flat == flat[0]):
+            # uniform mask: every row samples the same value (no need to touch ind0)
+            val = flat[0]
+            if mask_scale is None:
+                return np.full(self.N_eq, val)
+            out = np.zeros(self.N_eq, dtype=float)
+            for key, scaled in mask_scale.items():
+                if val == key:
+                    out[:] = scaled
+            return out
         rel = self.ind0 - self.grid.col_0
         if len(self.grid.shape) > len(mask.shape):
             subs = tuple(np.unravel_index(rel, self.grid.shape)[:len(mask.shape)])

@@ -28,6 +28,7 @@ from .constraint_functions import build_reference_epoch_matrix, reference_epoch_
 from .grid_functions import setup_averaging_ops, setup_avg_mask_ops, setup_grids, setup_z0_avg, \
     validate_by_dz_mask
 from .lin_op import lin_op
+from .assemble import describe
 from .solver import LSQSolver
 
 DEFAULTS = {'reference_epoch': 0, 'W_ctr': 1e4, 'return_fit_objects': False, 'mask_file': None,
@@ -56,16 +57,23 @@ class FitSystem:
     """The device-resident smooth_fit system: G = [G_data; Gc] (unweighted COO -> device CSR),
     Ip_c as a column map; rows re-weighted / re-selected per outer iteration."""
 
-    def __init__(self, G_data, Gc, keep_cols, n_full, device=0):
+    def __init__(self, G_data, Gc, keep_cols, n_full, device=0, structured=True):
         self.n_data, self.n_con = int(G_data.N_eq), int(Gc.N_eq)
         self.keep_cols = keep_cols
         self.n_full = int(n_full)
-        r1, c1, v1 = G_data.triplets()
-        r2, c2, v2 = Gc.triplets()
         self.solver = LSQSolver(device)
         self.solver.set_col_map(self.n_full, keep_cols)
-        self.solver.set_matrix_coo(self.n_data + self.n_con, self.n_full, np.concatenate([r1, r2 + self.n_data]),
-                                   np.concatenate([c1, c2]), np.concatenate([v1, v2]))
+        m = self.n_data + self.n_con
+        desc = describe(G_data, Gc) if structured else None
+        self.formation = 'stencil' if desc is not None else 'coo'
+        if desc is not None:       # rows generated on the device from the grids and stencils
+            grids, interp, coords, stencils, npts = desc
+            self.solver.set_matrix_stencil(m, self.n_full, grids, interp, coords, stencils, npts)
+        else:                      # generic lin_op: host triplets -> device CSR
+            r1, c1, v1 = G_data.triplets()
+            r2, c2, v2 = Gc.triplets()
+            self.solver.set_matrix_coo(m, self.n_full, np.concatenate([r1, r2 + self.n_data]),
+                                       np.concatenate([c1, c2]), np.concatenate([v1, v2]))
         self.stats = None
 
     def solve(self, row_weight, data_keep, rhs, x0=None, **opts):
@@ -200,7 +208,7 @@ def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grid
     return m0, sigma_extra, in_TSE, rs_data
 
 
-def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args):
+def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args, ru=None):
     """Output grids and fit statistics (smooth_fit.py:276-352)."""
     z0g, dzg = grids['z0'], grids['dz']
     m['z0'] = pc.grid.data().from_dict({'x': z0g.ctrs[1], 'y': z0g.ctrs[0], 'cell_area': z0g.cell_area,
@@ -216,8 +224,8 @@ def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args)
     m['extent'] = np.concatenate((z0g.bds[1], z0g.bds[0]))
     m['sensor_bias_grids'] = {}
     m['jitter_bias_grids'] = {}
-    Gc_csr = Gc.toCSR()
-    ru = Gc_csr.dot(m0)
+    if ru is None:               # unscaled constraint residuals Gc·m0 (device product when available)
+        ru = Gc.toCSR().dot(m0)
     rc = (1. / Ec) * ru          # TCinv_cov.dot(ru), smooth_fit.py:324-326
     for eq_type in ['d2z_dt2', 'grad2_z0', 'grad2_dzdt', 'grad2_PS']:
         if eq_type in Gc.TOC['rows']:
@@ -335,7 +343,8 @@ def smooth_fit(**kwargs):
             averaging_ops = setup_averaging_ops(grids['dz'], grids['dz'].col_N, args, grids['dz'].cell_area)
             averaging_ops.update(setup_z0_avg(grids, grids['dz'].col_N, args))
             averaging_ops.update(setup_avg_mask_ops(grids['dz'], G_data.col_N, args['avg_masks'], args['dzdt_lags']))
-            parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args)
+            ru = system.solver.spmv(m0[keep_cols])[system.n_data:]
+            parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args, ru=ru)
             tse = data.three_sigma_edit == 1
             r_data = data.z_est[tse] - data.z[tse]
             R['data'] = np.sum((r_data / data.sigma[tse]) ** 2)

@@ -68,6 +68,23 @@ class LSQSolver:
             self.n = int(n_full)
         self.n_full = int(n_full)
 
+    def set_matrix_stencil(self, m, n_full, grids, interp_grid, coords, stencils, npts, row_weight=None):
+        """Structured formation (lssurf_amd.assemble.describe output) — rows generated on device."""
+        from ._native import GridDesc, StencilDesc
+        ga = (GridDesc * len(grids))(*grids)
+        sa = (StencilDesc * max(len(stencils), 1))(*stencils)
+        ig = as_c(np.asarray(interp_grid, dtype=np.int32), np.int32)
+        py, px, pt = coords
+        w = None if row_weight is None else as_c(row_weight, np.float64)
+        self._check(self._L.lsq_set_matrix_stencil(self._h, int(m), int(n_full), len(grids), ctypes.cast(ga, ctypes.c_void_p),
+                                                   len(interp_grid), ptr(ig), int(npts), ptr(py), ptr(px), ptr(pt),
+                                                   len(stencils), ctypes.cast(sa, ctypes.c_void_p), ptr(w)),
+                    'lsq_set_matrix_stencil')
+        self.m = int(m)
+        if self.n is None:
+            self.n = int(n_full)
+        self.n_full = int(n_full)
+
     def set_row_weight(self, w):
         w = None if w is None else as_c(w, np.float64)
         self._check(self._L.lsq_set_row_weight(self._h, ptr(w)), 'lsq_set_row_weight')

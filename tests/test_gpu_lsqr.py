@@ -16,12 +16,12 @@ pytestmark = pytest.mark.gpu
 REL, ABS = 1e-6, 1e-4
 
 
-def _fit_system(name):
+def _fit_system(name, structured=True):
     g = golden(f'sys_{name}.npz')
     kw = golden_kwargs(g)
     S = LS.smooth_fit(data=golden_points(g), return_fit_objects=True, **kw)
     keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch'])
-    sysm = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N)
+    sysm = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, structured=structured)
     E_all = 1 / (1. / np.concatenate((S['Ed'], S['Ec'])))
     w = 1. / np.sqrt(E_all ** 2)
     rhs = np.zeros(S['G_data'].N_eq + S['Gc'].N_eq)
@@ -30,8 +30,10 @@ def _fit_system(name):
 
 
 @pytest.mark.parametrize('name', SYSTEMS)
-def test_device_formation_bitwise(gpu_available, name):
-    g, S, sysm, w, rhs = _fit_system(name)
+@pytest.mark.parametrize('structured', [True, False])
+def test_device_formation_bitwise(gpu_available, name, structured):
+    g, S, sysm, w, rhs = _fit_system(name, structured)
+    assert sysm.formation == ('stencil' if structured else 'coo')
     sysm.solver.set_row_weight(w)
     sysm.solver.set_row_mask(np.ones(sysm.n_data + sysm.n_con, bool))
     A = sysm.solver.get_csr()
@@ -234,3 +236,20 @@ def test_dense_precond_stiff_kat_system(gpu_available):
     fs.close()
     xs = dense.ls_solve_dense(A, w * rhs)
     assert np.linalg.norm(x - xs) / np.linalg.norm(xs) < 1e-9
+
+
+def test_stencil_formation_equals_coo_formation_t64(gpu_available):
+    """64x64x12, 8 k points: device-generated rows == host-triplet rows, bit for bit."""
+    from lssurf_amd import synthetic
+    D, kw = synthetic.points('t64')
+    S = LS.smooth_fit(data=D, return_fit_objects=True, VERBOSE=False, **kw)
+    keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch'])
+    mats = []
+    for structured in (True, False):
+        fs = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, structured=structured)
+        mats.append(fs.solver.get_csr())
+        fs.close()
+    a, b = mats
+    np.testing.assert_array_equal(a.indptr, b.indptr)
+    np.testing.assert_array_equal(a.indices, b.indices)
+    np.testing.assert_array_equal(a.data, b.data)

@@ -108,3 +108,19 @@ def test_out_of_scope_options_raise():
     with pytest.raises(NotImplementedError):
         LS.smooth_fit(data=D, W={'x': 1e3, 'y': 1e3, 't': 1}, ctr={'x': 0, 'y': 0, 't': 0},
                       spacing={'z0': 100, 'dz': 100, 'dt': .25}, E_RMS={'d2z0_dx2': 1}, bias_params=['cycle'])
+
+
+def test_structured_description_of_smooth_fit_system():
+    from lssurf_amd import assemble, synthetic
+    D, kw = synthetic.points('t64')
+    S = LS.smooth_fit(data=D, return_fit_objects=True, VERBOSE=False, **kw)
+    d = assemble.describe(S['G_data'], S['Gc'])
+    assert d is not None
+    grids, interp, coords, stencils, npts = d
+    assert len(grids) == 2 and interp == [0, 1] and npts == D.size
+    assert sum(s.n_eq for s in stencils) == S['Gc'].N_eq
+    assert not S['Gc'].materialized          # nothing was built on the host
+    # values changed by data -> no structure -> COO path
+    op = LS.lin_op(S['grids']['dz'], name='dzdt_lag1').dzdt(lag=1)
+    op.normalize_by_unit_product()
+    assert op.parts is None
