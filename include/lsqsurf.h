@@ -144,6 +144,38 @@ int lsq_iterate(lsq_handle* h, const double* b, int64_t iters, const lsq_opts* o
 int lsq_sigma_x(lsq_handle* h, double* E);
 int lsq_get_rinv(lsq_handle* h, double* Rinv);
 
+/* ---- multi-GPU (one process per GPU) --------------------------------------
+ * lsq_dist_unique_id: rank 0 creates the 128-byte RCCL id; the caller broadcasts it (any
+ * transport); every rank then calls lsq_create_dist.  Each rank forms only the rows it owns
+ * (lsq_set_col_map + lsq_set_matrix_* with GLOBAL column ids), reads which columns its rows
+ * reference, and installs its layout: col_local maps every global column to a local id
+ * ([0, n_own) owned, [n_own, n_local) ghosts grouped by owning peer, -1 unused); for each
+ * peer, send_idx lists the owned local columns that peer holds as ghosts (in the order of the
+ * peer's ghost slots) and recv_cnt the number of ghosts it owns.  lsq_solve / lsq_iterate then
+ * run one LSQR over all ranks: halo exchange of ghost v before A·v, reverse halo of ghost
+ * partial sums after Aᵀu, RCCL all-reduce of the scalar norms; x_inout receives the owned
+ * columns (length n_own). */
+int lsq_dist_unique_id(uint8_t* id128);
+lsq_handle* lsq_create_dist(int32_t device, int32_t rank, int32_t nranks, const uint8_t* id128);
+int lsq_dist_referenced_cols(lsq_handle* h, uint8_t* flags);
+int lsq_dist_set_layout(lsq_handle* h, const int32_t* col_local, int64_t n_local, int64_t n_own,
+                        int32_t n_peers, const int32_t* peers, const int64_t* send_cnt,
+                        const int32_t* send_idx, const int64_t* recv_cnt);
+
+/* Virtual ranks: the same distributed solve with every rank of the partition in THIS process
+ * on one device (exchanges become device copies).  Configure each rank's handle exactly as a
+ * real rank (lsq_set_col_map, lsq_set_matrix_*, lsq_dist_referenced_cols,
+ * lsq_dist_set_layout), then solve all ranks at once; b / x are per-rank arrays. */
+typedef struct lsq_vgroup lsq_vgroup;
+lsq_vgroup* lsq_vgroup_create(int32_t device, int32_t nranks);
+lsq_handle* lsq_vgroup_rank(lsq_vgroup* g, int32_t rank);
+int lsq_vgroup_solve(lsq_vgroup* g, const double* const* b, double* const* x, const lsq_opts* o,
+                     lsq_stats* s);
+int lsq_vgroup_iterate(lsq_vgroup* g, const double* const* b, int64_t iters, const lsq_opts* o,
+                       lsq_stats* s);
+const char* lsq_vgroup_last_error(lsq_vgroup* g);
+void lsq_vgroup_destroy(lsq_vgroup* g);
+
 /* Bench / profiling hooks.  lsq_profile_kernels times each iteration kernel in isolation
  * (reps launches each, HIP events on the handle's stream): ms4 = {x/w+SpMV, SpMTV, beta reduce,
  * rotation}.  It clobbers the iteration state.  lsq_sell_info: {m, n, nnz, SELL entries of A,

@@ -45,7 +45,9 @@ class LsqStats(ctypes.Structure):
 EXPORTS = ['lsq_default_opts', 'lsq_create', 'lsq_destroy', 'lsq_last_error', 'lsq_set_col_map',
            'lsq_set_matrix_coo', 'lsq_set_matrix_stencil', 'lsq_set_row_weight', 'lsq_set_row_mask', 'lsq_shape', 'lsq_get_csr',
            'lsq_solve', 'lsq_spmv', 'lsq_iterate', 'lsq_profile_kernels', 'lsq_sell_info', 'lsq_sigma_x',
-           'lsq_get_rinv',
+           'lsq_get_rinv', 'lsq_dist_unique_id', 'lsq_create_dist', 'lsq_dist_referenced_cols',
+           'lsq_dist_set_layout', 'lsq_vgroup_create', 'lsq_vgroup_rank', 'lsq_vgroup_solve', 'lsq_vgroup_iterate',
+           'lsq_vgroup_last_error', 'lsq_vgroup_destroy',
            'tri_upper_solve_csr', 'tri_upper_inv_csr', 'tri_upper_rowrss_csr', 'tri_last_error']
 
 _lib = None
@@ -79,6 +81,16 @@ def load():
         'lsq_sell_info': ([P, P], ctypes.c_int),
         'lsq_sigma_x': ([P, P], ctypes.c_int),
         'lsq_get_rinv': ([P, P], ctypes.c_int),
+        'lsq_dist_unique_id': ([P], ctypes.c_int),
+        'lsq_create_dist': ([i32, i32, i32, P], P),
+        'lsq_dist_referenced_cols': ([P, P], ctypes.c_int),
+        'lsq_dist_set_layout': ([P, P, i64, i64, i32, P, P, P, P], ctypes.c_int),
+        'lsq_vgroup_create': ([i32, i32], P),
+        'lsq_vgroup_rank': ([P, i32], P),
+        'lsq_vgroup_solve': ([P, P, P, P, P], ctypes.c_int),
+        'lsq_vgroup_iterate': ([P, P, i64, P, P], ctypes.c_int),
+        'lsq_vgroup_last_error': ([P], ctypes.c_char_p),
+        'lsq_vgroup_destroy': ([P], None),
         'tri_upper_solve_csr': ([i32, i64, P, P, P, P, P], ctypes.c_int),
         'tri_upper_inv_csr': ([i32, i64, P, P, P, i64, ctypes.c_float, P, P, P, P], ctypes.c_int),
         'tri_upper_rowrss_csr': ([i32, i64, P, P, P, P], ctypes.c_int),

@@ -54,7 +54,8 @@ def build(force=False, verbose=False):
         list(ex.map(run, jobs))
     objs = [os.path.join(OBJ, s.replace('.hip', '.o')) for s in SOURCES]
     if force or jobs or not os.path.exists(LIB):
-        run([_hipcc(), '-shared', f'--offload-arch={ARCH}', '-o', LIB, *objs])
+        run([_hipcc(), '-shared', f'--offload-arch={ARCH}', '-o', LIB, *objs, '-L/opt/rocm/lib', '-lrccl',
+             '-Wl,-rpath,/opt/rocm/lib'])
     return LIB
 
 

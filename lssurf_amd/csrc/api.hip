@@ -240,6 +240,13 @@ int lsq_solve(lsq_handle* h, const double* b, double* x_inout, const lsq_opts* o
         if (!o) o = &d;
         if (o->method != 0) return fail(S, "lsq_solve: only method 0 (LSQR) is implemented");
         if (o->precond < 0 || o->precond > 2) return fail(S, "lsq_solve: precond must be 0, 1 or 2");
+        if (S.dist) {
+            if (S.virt) return fail(S, "lsq_solve: a virtual rank solves through lsq_vgroup_solve");
+            lsq::Group G;
+            G.ranks = {&S};
+            double* xs[1] = {x_inout};
+            return lsq::group_solve(G, &b, xs, *o, s);
+        }
         return lsq::lsqr_solve(S, b, x_inout, *o, s);
     });
 }
@@ -250,6 +257,12 @@ int lsq_iterate(lsq_handle* h, const double* b, int64_t iters, const lsq_opts* o
         lsq_opts d;
         lsq_default_opts(&d);
         if (!o) o = &d;
+        if (S.dist) {
+            if (S.virt) return fail(S, "lsq_iterate: a virtual rank iterates through lsq_vgroup_iterate");
+            lsq::Group G;
+            G.ranks = {&S};
+            return lsq::group_iterate(G, &b, iters, *o, s);
+        }
         return lsq::lsqr_iterate(S, b, iters, *o, s);
     });
 }
@@ -271,6 +284,81 @@ int lsq_sell_info(lsq_handle* h, int64_t* out6) {
         out6[4] = S.AT.nent;
         out6[5] = (int64_t)(S.G.rp.bytes() + S.G.ci.bytes() + S.G.val.bytes() + S.GT.rp.bytes() + S.GT.ci.bytes() +
                             S.GT.val.bytes() + S.A.ci.bytes() + S.A.val.bytes() + S.AT.ci.bytes() + S.AT.val.bytes());
+        return 0;
+    });
+}
+
+int lsq_dist_unique_id(uint8_t* id) {
+    if (!id) return -1;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return -3;
+    std::memcpy(id, &u, sizeof(u));
+    return 0;
+}
+
+lsq_handle* lsq_create_dist(int32_t device, int32_t rank, int32_t nranks, const uint8_t* id) {
+    if (!id || nranks < 1 || rank < 0 || rank >= nranks) return nullptr;
+    lsq_handle* h = lsq_create(device);
+    if (!h) return nullptr;
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    if (ncclCommInitRank(&h->sys.comm, nranks, u, rank) != ncclSuccess) {
+        h->sys.comm = nullptr;
+        lsq_destroy(h);
+        return nullptr;
+    }
+    h->sys.rank = rank;
+    h->sys.nranks = nranks;
+    return h;
+}
+
+int lsq_dist_referenced_cols(lsq_handle* h, uint8_t* flags) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p || !flags) return fail(S, "lsq_dist_referenced_cols: no matrix / null output");
+        if (S.dist) return fail(S, "lsq_dist_referenced_cols: layout already set");
+        lsq::referenced_cols(S, flags);
+        return 0;
+    });
+}
+
+int lsq_dist_set_layout(lsq_handle* h, const int32_t* col_local, int64_t n_local, int64_t n_own, int32_t n_peers,
+                        const int32_t* peers, const int64_t* send_cnt, const int32_t* send_idx,
+                        const int64_t* recv_cnt) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.comm && !S.virt)
+            return fail(S, "lsq_dist_set_layout: handle has no communicator (use lsq_create_dist / lsq_vgroup)");
+        if (!S.G.rp.p || S.dist) return fail(S, "lsq_dist_set_layout: needs a formed matrix, once");
+        if (!col_local || n_own < 0 || n_own > n_local || n_peers < 0) return fail(S, "lsq_dist_set_layout: bad args");
+        S.peers.assign(peers, peers + n_peers);
+        S.send_cnt.assign(send_cnt, send_cnt + n_peers);
+        S.recv_cnt.assign(recv_cnt, recv_cnt + n_peers);
+        S.send_off.assign(n_peers, 0);
+        S.recv_off.assign(n_peers, 0);
+        int64_t ts = 0, tr = 0;
+        for (int k = 0; k < n_peers; ++k) {
+            if (peers[k] < 0 || peers[k] >= S.nranks || peers[k] == S.rank)
+                return fail(S, "lsq_dist_set_layout: bad peer rank");
+            S.send_off[k] = ts;
+            S.recv_off[k] = tr;
+            ts += send_cnt[k];
+            tr += recv_cnt[k];
+        }
+        if (tr != n_local - n_own) return fail(S, "lsq_dist_set_layout: receive counts must cover the ghosts");
+        for (int64_t k = 0; k < ts; ++k)
+            if (send_idx[k] < 0 || send_idx[k] >= n_own) return fail(S, "lsq_dist_set_layout: send index not owned");
+        lsq::graph_cache_drop(&S);
+        lsq::relabel_columns(S, col_local, n_local);
+        S.n_own = n_own;
+        S.send_idx.alloc(ts);
+        S.send_idx.upload(send_idx, ts, S.stream);
+        S.sbuf.alloc(std::max<int64_t>(ts, 1));
+        S.rbuf.alloc(std::max<int64_t>(ts, 1));
+        S.gsum.alloc(8);
+        S.gsum.zero(S.stream);
+        HIP_CHECK(hipStreamSynchronize(S.stream));
+        S.dist = true;
+        S.u = lsq::DBuf<double>();
+        S.vb0 = lsq::DBuf<double>();   // workspace re-sized on first use
         return 0;
     });
 }
@@ -303,6 +391,93 @@ int lsq_spmv(lsq_handle* h, int32_t trans, const double* x, double* y) {
         dy.download(y, nout, S.stream);
         HIP_CHECK(hipStreamSynchronize(S.stream));
         return 0;
+    });
+}
+
+struct lsq_vgroup {
+    std::vector<lsq_handle*> h;
+    hipStream_t stream = nullptr;
+    lsq::Group G;
+    std::string err;
+};
+
+lsq_vgroup* lsq_vgroup_create(int32_t device, int32_t nranks) {
+    if (nranks < 1) return nullptr;
+    auto* g = new lsq_vgroup();
+    for (int r = 0; r < nranks; ++r) {
+        lsq_handle* h = lsq_create(device);
+        if (!h) {
+            lsq_vgroup_destroy(g);
+            return nullptr;
+        }
+        h->sys.virt = true;
+        h->sys.rank = r;
+        h->sys.nranks = nranks;
+        if (r == 0) {
+            g->stream = h->sys.stream;
+        } else {   // every virtual rank runs on rank 0's stream: exchanges need no extra sync
+            (void)hipStreamDestroy(h->sys.stream);
+            h->sys.stream = g->stream;
+            h->sys.own_stream = false;
+        }
+        g->h.push_back(h);
+    }
+    return g;
+}
+
+lsq_handle* lsq_vgroup_rank(lsq_vgroup* g, int32_t rank) {
+    return (g && rank >= 0 && rank < (int)g->h.size()) ? g->h[rank] : nullptr;
+}
+
+const char* lsq_vgroup_last_error(lsq_vgroup* g) { return g ? g->err.c_str() : "null group"; }
+
+void lsq_vgroup_destroy(lsq_vgroup* g) {
+    if (!g) return;
+    for (int r = (int)g->h.size() - 1; r >= 0; --r) lsq_destroy(g->h[r]);   // rank 0 owns the stream
+    delete g;
+}
+
+}  // extern "C"
+
+template <class F>
+static int vguarded(lsq_vgroup* g, F&& f) {
+    if (!g || g->h.empty()) return -1;
+    g->err.clear();
+    try {
+        HIP_CHECK(hipSetDevice(g->h[0]->sys.device));
+        if (g->G.ranks.empty()) {
+            for (auto* h : g->h) {
+                if (!h->sys.dist) throw std::invalid_argument("every virtual rank needs lsq_dist_set_layout first");
+                g->G.ranks.push_back(&h->sys);
+            }
+            g->G.virt = true;
+            lsq::group_prepare_virtual(g->G);
+        }
+        return f(g->G);
+    } catch (const std::invalid_argument& e) {
+        g->err = e.what();
+        return -2;
+    } catch (const std::exception& e) {
+        g->err = e.what();
+        return -3;
+    }
+}
+
+extern "C" {
+
+int lsq_vgroup_solve(lsq_vgroup* g, const double* const* b, double* const* x, const lsq_opts* o, lsq_stats* s) {
+    return vguarded(g, [&](lsq::Group& G) {
+        lsq_opts d;
+        lsq_default_opts(&d);
+        return lsq::group_solve(G, b, x, o ? *o : d, s);
+    });
+}
+
+int lsq_vgroup_iterate(lsq_vgroup* g, const double* const* b, int64_t iters, const lsq_opts* o, lsq_stats* s) {
+    return vguarded(g, [&](lsq::Group& G) {
+        lsq_opts d;
+        lsq_default_opts(&d);
+        return lsq::group_iterate(G, b, iters, o ? *o : d, s);
     });
 }
 

@@ -237,15 +237,23 @@ __global__ __launch_bounds__(BLOCK) void k_rowscale(int64_t m, const double* __r
 }
 
 // Jacobi column scaling: cs_j = 1/||(diag(rs) G)_{:,j}||  (1 for an empty column).
+// raw = 1 stores the squared norm (distributed: summed across ranks before finishing).
 __global__ __launch_bounds__(BLOCK) void k_colnorm(int64_t n, const int64_t* __restrict__ trp,
                                                    const int32_t* __restrict__ tci, const double* __restrict__ tval,
-                                                   const double* __restrict__ rs, double* __restrict__ cs) {
+                                                   const double* __restrict__ rs, double* __restrict__ cs, int raw) {
     for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLOCK) {
         double s = 0.0;
         for (int64_t e = trp[j]; e < trp[j + 1]; ++e) {
             const double a = tval[e] * rs[tci[e]];
             s += a * a;
         }
+        cs[j] = raw ? s : (s > 0.0 ? 1.0 / sqrt(s) : 1.0);
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_cs_finish(int64_t n, double* __restrict__ cs) {
+    for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLOCK) {
+        const double s = cs[j];
         cs[j] = s > 0.0 ? 1.0 / sqrt(s) : 1.0;
     }
 }
@@ -261,6 +269,39 @@ __global__ __launch_bounds__(BLOCK) void k_csr_spmv(int64_t rows, const int64_t*
         double acc = 0.0;
         for (int64_t e = rp[r]; e < rp[r + 1]; ++e) acc += val[e] * x[ci[e]];
         y[r] = acc;
+    }
+}
+
+// distributed layout: mark referenced columns; relabel columns to local ids and re-sort rows
+__global__ __launch_bounds__(BLOCK) void k_flag_cols(int64_t nnz, const int32_t* __restrict__ ci,
+                                                     uint8_t* __restrict__ flags) {
+    for (int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x; e < nnz; e += (int64_t)gridDim.x * BLOCK)
+        flags[ci[e]] = 1;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_relabel_rows(int64_t m, const int64_t* __restrict__ rp,
+                                                        int32_t* __restrict__ ci, double* __restrict__ val,
+                                                        const int32_t* __restrict__ map,
+                                                        unsigned long long* __restrict__ bad) {
+    for (int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x; r < m; r += (int64_t)gridDim.x * BLOCK) {
+        const int64_t b = rp[r], L = rp[r + 1] - b;
+        for (int64_t k = 0; k < L; ++k) {
+            const int32_t c = map[ci[b + k]];
+            if (c < 0) atomicAdd(bad, 1ull);
+            ci[b + k] = c;
+        }
+        for (int64_t i = 1; i < L; ++i) {
+            const int32_t kc = ci[b + i];
+            const double kv = val[b + i];
+            int64_t j = i - 1;
+            while (j >= 0 && ci[b + j] > kc) {
+                ci[b + j + 1] = ci[b + j];
+                val[b + j + 1] = val[b + j];
+                --j;
+            }
+            ci[b + j + 1] = kc;
+            val[b + j + 1] = kv;
+        }
     }
 }
 
@@ -398,20 +439,31 @@ void finish_formation(System& S) {
     HIP_CHECK(hipStreamSynchronize(st));
 }
 
-void refresh_scaling(System& S, int precond) {
+// Scaling is applied in three phases so a distributed group can exchange column norms between
+// them: (1) row scale + (raw) column norms, (2) [dist: reverse halo, finish, forward halo],
+// (3) fill the SELL values.
+void scaling_rows_colnorm(System& S, int precond, bool raw) {
     hipStream_t st = S.stream;
     const int64_t m = S.G.m, n = S.G.n;
-    if (!S.rs_dirty && S.cs_mode == precond) return;
     hipLaunchKernelGGL(k_rowscale, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, S.roww.p, S.rowkeep.p, S.rs.p);
     KERNEL_CHECK();
     S.dense_valid = false;   // the dense factor depends on the row scaling
-    if (precond == 1) {
+    if (precond == 1)
         hipLaunchKernelGGL(k_colnorm, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, S.GT.rp.p, S.GT.ci.p, S.GT.val.p,
-                           S.rs.p, S.cs.p);
-    } else {
+                           S.rs.p, S.cs.p, raw ? 1 : 0);
+    else
         hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, 1.0, S.cs.p);
-    }
     KERNEL_CHECK();
+}
+
+void scaling_finish_cs(System& S) {
+    hipLaunchKernelGGL(k_cs_finish, dim3(grid_for(S.n_own)), dim3(BLOCK), 0, S.stream, S.n_own, S.cs.p);
+    KERNEL_CHECK();
+}
+
+void scaling_fill_values(System& S, int precond) {
+    hipStream_t st = S.stream;
+    const int64_t m = S.G.m, n = S.G.n;
     hipLaunchKernelGGL(k_sell_vals, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, S.G.rp.p, S.G.ci.p, S.G.val.p, S.rs.p,
                        S.cs.p, 0, S.A.sp.p, S.A.val.p);
     KERNEL_CHECK();
@@ -423,14 +475,52 @@ void refresh_scaling(System& S, int precond) {
     S.iter_ready = false;
 }
 
+bool scaling_stale(const System& S, int precond) { return S.rs_dirty || S.cs_mode != precond; }
+
+void refresh_scaling(System& S, int precond) {
+    if (!scaling_stale(S, precond)) return;
+    if (S.dist) throw std::logic_error("refresh_scaling: distributed systems refresh through their group");
+    scaling_rows_colnorm(S, precond, false);
+    scaling_fill_values(S, precond);
+}
+
 void csr_spmv(System& S, int trans, const double* dx, double* dy) {
     const Csr& C = trans ? S.GT : S.G;
     hipLaunchKernelGGL(k_csr_spmv, dim3(grid_for(C.m)), dim3(BLOCK), 0, S.stream, C.m, C.rp.p, C.ci.p, C.val.p, dx, dy);
     KERNEL_CHECK();
 }
 
+void referenced_cols(System& S, uint8_t* h_flags) {
+    DBuf<uint8_t> f(std::max<int64_t>(S.G.n, 1));
+    f.zero(S.stream);
+    hipLaunchKernelGGL(k_flag_cols, dim3(grid_for(S.G.nnz)), dim3(BLOCK), 0, S.stream, S.G.nnz, S.G.ci.p, f.p);
+    KERNEL_CHECK();
+    f.download(h_flags, S.G.n, S.stream);
+    HIP_CHECK(hipStreamSynchronize(S.stream));
+}
+
+void relabel_columns(System& S, const int32_t* h_map, int64_t n_local) {
+    DBuf<int32_t> map(std::max<int64_t>(S.G.n, 1));
+    map.upload(h_map, S.G.n, S.stream);
+    DBuf<unsigned long long> bad(1);
+    bad.zero(S.stream);
+    hipLaunchKernelGGL(k_relabel_rows, dim3(grid_for(S.G.m)), dim3(BLOCK), 0, S.stream, S.G.m, S.G.rp.p, S.G.ci.p,
+                       S.G.val.p, map.p, bad.p);
+    KERNEL_CHECK();
+    unsigned long long h = 0;
+    HIP_CHECK(hipMemcpyAsync(&h, bad.p, sizeof(h), hipMemcpyDeviceToHost, S.stream));
+    HIP_CHECK(hipStreamSynchronize(S.stream));
+    if (h) throw std::invalid_argument("lsq_dist_set_layout: a referenced column has no local index");
+    S.G.n = n_local;
+    S.GT = Csr{};
+    S.A = Sell{};
+    S.AT = Sell{};
+    finish_formation(S);
+}
+
 System::~System() {
-    if (stream) (void)hipStreamDestroy(stream);
+    if (comm) (void)ncclCommDestroy(comm);
+    if (stream && own_stream) (void)hipStreamDestroy(stream);
 }
 
 }  // namespace lsq

@@ -166,14 +166,15 @@ __device__ double reduce_parts(const double* part, int nparts) {
 // ---- β: 1-block kernel --------------------------------------------------------------------------
 // mode 0: iteration; mode 1: init (also bnorm from part_b)
 __global__ __launch_bounds__(BLOCK) void k_beta(LsqState* st, const double* part_u, int nu,
-                                                const double* part_b, int nb, int mode) {
+                                                const double* part_b, int nb, int mode, const double* gs) {
     if (mode == 0 && st->stop) {
         if (threadIdx.x == 0) st->finished = 1;   // the final x/w update has been applied
         return;
     }
-    const double su = reduce_parts(part_u, nu);
+    // gs: sums already reduced (and all-reduced across ranks): gs[0] = Σu², gs[3] = Σb²
+    const double su = gs ? gs[0] : reduce_parts(part_u, nu);
     double sb = 0.0;
-    if (mode == 1) sb = reduce_parts(part_b, nb);
+    if (mode == 1) sb = gs ? gs[3] : reduce_parts(part_b, nb);
     if (threadIdx.x) return;
     const double beta = sqrt(su);
     st->beta = beta;
@@ -211,10 +212,11 @@ __device__ void sym_ortho(double a, double b, double& c, double& s, double& r) {
 // ---- α, rotation, norm estimates, stopping rules: 1-block kernel ----------------------------
 // mode 1: init (rhobar = α, φ̄ = β ...); mode 0: iteration
 __global__ __launch_bounds__(BLOCK) void k_givens(LsqState* st, const double* part_v, int nv,
-                                                  const double* part_w, int nw, int mode) {
+                                                  const double* part_w, int nw, int mode, const double* gs) {
     if (mode == 0 && st->stop) return;
-    const double sv = reduce_parts(part_v, nv);
-    const double sw = reduce_parts(part_w, nw);
+    // gs: gs[1] = Σw², gs[2] = Σṽ² (reduced across ranks)
+    const double sv = gs ? gs[2] : reduce_parts(part_v, nv);
+    const double sw = gs ? gs[1] : reduce_parts(part_w, nw);
     if (threadIdx.x) return;
     const double eps = 2.220446049250313e-16;
     if (!st->skip_v) {
@@ -313,17 +315,59 @@ __global__ __launch_bounds__(BLOCK) void k_scale(int64_t n, const double* __rest
         out[j] = divide ? a[j] / cs[j] : a[j] * cs[j];
 }
 
+// ---- distributed helpers ---------------------------------------------------------------------
+// gs[slot_a] = Σ part_a, gs[slot_b] = Σ part_b (rank-local, deterministic), before the all-reduce
+__global__ __launch_bounds__(BLOCK) void k_red_parts(const double* part_a, int na, int slot_a, const double* part_b,
+                                                     int nb, int slot_b, double* gs) {
+    const double a = reduce_parts(part_a, na);
+    double b = 0.0;
+    if (part_b) b = reduce_parts(part_b, nb);
+    if (threadIdx.x == 0) {
+        gs[slot_a] = a;
+        if (part_b) gs[slot_b] = b;
+    }
+}
+
+// ṽ'_j = t_j/β − β ṽ_j/α over owned columns (after the reverse halo), Σṽ'²
+__global__ __launch_bounds__(BLOCK) void k_vepi(const LsqState* __restrict__ st, int64_t n,
+                                                const double* __restrict__ t, const double* __restrict__ vin,
+                                                double* __restrict__ vout, double* part_v) {
+    if (st->stop) return;
+    const double ib = st->inv_beta, beta = st->beta, ia = st->inv_alpha;
+    const bool skip = st->skip_v;
+    double sv = 0.0;
+    for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLOCK) {
+        const double vn = skip ? vin[j] : t[j] * ib - beta * (vin[j] * ia);
+        vout[j] = vn;
+        sv += vn * vn;
+    }
+    store_partial(sv, part_v, blockIdx.x);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_pack(int64_t cnt, const int32_t* __restrict__ idx,
+                                                const double* __restrict__ src, double* __restrict__ dst) {
+    for (int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x; k < cnt; k += (int64_t)gridDim.x * BLOCK)
+        dst[k] = src[idx[k]];
+}
+
+__global__ __launch_bounds__(BLOCK) void k_scatter_add(int64_t cnt, const int32_t* __restrict__ idx,
+                                                       const double* __restrict__ src, double* __restrict__ dst) {
+    for (int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x; k < cnt; k += (int64_t)gridDim.x * BLOCK)
+        dst[idx[k]] += src[k];
+}
+
 struct Grids {
-    int gA, gT, gX, gR, gRT;
+    int gA, gT, gX, gR, gRT, gE;
 };
 
 Grids grids_for(const System& S) {
     Grids g;
     g.gA = (int)std::min<int64_t>(std::max<int64_t>((S.A.nslices + 3) / 4, 1), NPART);
     g.gT = (int)std::min<int64_t>(std::max<int64_t>((S.AT.nslices + 3) / 4, 1), NPART);
-    g.gX = grid_for(S.G.n, BLOCK * 4, NPART);
+    g.gX = grid_for(S.ncols_own(), BLOCK * 4, NPART);
     g.gR = grid_for(S.G.n, 4, NPART);        // k_gemv_upper: one wave per row
     g.gRT = grid_for(S.G.n, BLOCK, NPART);   // k_gemvT_upper: one thread per column
+    g.gE = grid_for(S.ncols_own(), BLOCK * 4, NPART);
     return g;
 }
 
@@ -362,26 +406,26 @@ void launch_iteration(System& S, const Grids& g, int p, int precond) {
     hipLaunchKernelGGL(k_xw_spmv, dim3(g.gX + g.gA), dim3(BLOCK), 0, st, S.st.p, g.gX, S.G.n, S.y.p, S.w.p, vt,
                        dense ? S.zt.p : vt, dense ? 0 : 1, S.G.m, S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p, S.u.p,
                        S.part_u.p, S.part_w.p);
-    hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gA, S.part_b.p, 0, 0);
+    hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gA, S.part_b.p, 0, 0, nullptr);
     if (dense) {
         hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, S.G.n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
                            S.AT.val.p, S.u.p, vt, S.tt.p, S.part_v.p, 1);
         hipLaunchKernelGGL(k_gemvT_upper, dim3(g.gRT), dim3(BLOCK), 0, st, S.dRi.p, S.G.n, S.dense_ld, S.tt.p, S.st.p,
                            1, vt, vo, S.part_v.p);
-        hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gRT, S.part_w.p, g.gX, 0);
+        hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gRT, S.part_w.p, g.gX, 0, nullptr);
     } else {
         hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, S.G.n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
                            S.AT.val.p, S.u.p, vt, vo, S.part_v.p, 0);
-        hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gT, S.part_w.p, g.gX, 0);
+        hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gT, S.part_w.p, g.gX, 0, nullptr);
     }
 }
 
 // final x/w update of a solve that stopped on the last iteration of a batch (newest ṽ in vb0)
 void launch_flush(System& S, const Grids& g) {
-    hipLaunchKernelGGL(k_xw_spmv, dim3(g.gX + g.gA), dim3(BLOCK), 0, S.stream, S.st.p, g.gX, S.G.n, S.y.p, S.w.p,
+    hipLaunchKernelGGL(k_xw_spmv, dim3(g.gX + g.gA), dim3(BLOCK), 0, S.stream, S.st.p, g.gX, S.ncols_own(), S.y.p, S.w.p,
                        S.vb0.p, S.vb0.p, 1, S.G.m, S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p, S.u.p, S.part_u.p,
                        S.part_w.p);
-    hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, S.stream, S.st.p, S.part_u.p, g.gA, S.part_b.p, 0, 0);
+    hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, S.stream, S.st.p, S.part_u.p, g.gA, S.part_b.p, 0, 0, nullptr);
     KERNEL_CHECK();
 }
 
@@ -424,7 +468,7 @@ void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts&
     hipLaunchKernelGGL(k_init_u, dim3(g.gA), dim3(BLOCK), 0, st, m, S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p,
                        S.rs.p, db.p, gather0, S.u.p, S.bw.p, S.part_u.p, S.part_b.p);
     KERNEL_CHECK();
-    hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gA, S.part_b.p, g.gA, 1);
+    hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gA, S.part_b.p, g.gA, 1, nullptr);
     KERNEL_CHECK();
     S.vb1.zero(st);
     int nv = g.gT;
@@ -439,7 +483,7 @@ void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts&
                            S.AT.val.p, S.u.p, S.vb1.p, S.vb0.p, S.part_v.p, 0);
     }
     KERNEL_CHECK();
-    hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, nv, S.part_w.p, g.gX, 1);
+    hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, nv, S.part_w.p, g.gX, 1, nullptr);
     KERNEL_CHECK();
     hipLaunchKernelGGL(k_init_w, dim3(g.gX), dim3(BLOCK), 0, st, S.st.p, n, S.vb0.p, h_x0 ? dy0.p : nullptr, S.w.p,
                        S.y.p, S.part_w.p);
@@ -626,10 +670,10 @@ void lsqr_profile(System& S, int reps, double* ms_out /* [4]: xw_spmv, spmtv, be
                                        S.AT.sp.p, S.AT.ci.p, S.AT.val.p, S.u.p, S.vb0.p, S.vb1.p, S.part_v.p, 0);
                 else if (k == 2)
                     hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, S.stream, S.st.p, S.part_u.p, g.gA,
-                                       S.part_b.p, 0, 2);
+                                       S.part_b.p, 0, 2, nullptr);
                 else
                     hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, S.stream, S.st.p, S.part_v.p, g.gT,
-                                       S.part_w.p, g.gX, 2);
+                                       S.part_w.p, g.gX, 2, nullptr);
             }
             HIP_CHECK(hipEventRecord(e1, S.stream));
             HIP_CHECK(hipEventSynchronize(e1));
@@ -662,5 +706,7 @@ void lsqr_get_rinv(System& S, double* h_Ri) {
                                hipMemcpyDeviceToHost, S.stream));
     HIP_CHECK(hipStreamSynchronize(S.stream));
 }
+
+#include "lsqr_dist.inc"
 
 }  // namespace lsq

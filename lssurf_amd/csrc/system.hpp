@@ -11,8 +11,12 @@
 // The SELL copies are what the LSQR iteration streams; G/GT keep the unweighted values so
 // row weights / masks / preconditioner changes only re-fill values (no re-formation).
 #pragma once
-#include <string>
+#include <rccl/rccl.h>
 
+#include <string>
+#include <vector>
+
+#include "../../include/lsqsurf.h"
 #include "common.hpp"
 
 namespace lsq {
@@ -72,6 +76,22 @@ struct System {
     int64_t dense_ld = 0;
     bool dense_valid = false;
 
+    // distributed layout (y-slab partition, one rank per GPU): columns [0, n_own) are owned,
+    // [n_own, G.n) are ghosts grouped by owner; rows are all owned.  One exchange plan serves
+    // the forward halo (owned values -> peers' ghost slots) and the reverse halo (ghost partial
+    // sums -> owners, added in peer order).
+    bool dist = false;
+    bool virt = false;              // in-process virtual rank (shares device + stream with its group)
+    bool own_stream = true;
+    int rank = 0, nranks = 1;
+    ncclComm_t comm = nullptr;
+    int64_t n_own = 0;
+    std::vector<int> peers;
+    std::vector<int64_t> send_cnt, send_off, recv_cnt, recv_off;
+    DBuf<int32_t> send_idx;         // concatenated by peer: owned local column indices
+    DBuf<double> sbuf, rbuf;        // packed forward values / received reverse partials
+    DBuf<double> gsum;              // [0] Σu², [1] Σw², [2] Σṽ², [3] Σb² (all-reduced)
+
     // LSQR workspace
     DBuf<double> u, vb0, vb1, w, y, bw, zt, tt;
     DBuf<double> part_u, part_v, part_w, part_b;
@@ -79,14 +99,35 @@ struct System {
     bool iter_ready = false;   // lsq_iterate state initialised
     int iter_parity = 0;
 
+    int64_t ncols_own() const { return dist ? n_own : G.n; }   // columns whose x this rank solves
     ~System();
 };
+
+// A set of ranks solved together.  RCCL mode: the one System of this process (peers live in
+// other processes).  Virtual mode: every rank of the problem in this process, on one device and
+// one stream, exchanging by device copies — the same kernels and plans, testable on one GPU.
+struct Group {
+    std::vector<System*> ranks;
+    bool virt = false;
+    DBuf<double*> gs_ptrs;   // virtual all-reduce: device array of the ranks' gsum pointers
+};
+
+// dist (build.hip / lsqr.hip)
+void group_prepare_virtual(Group& G);
+int group_solve(Group& G, const double* const* h_b, double* const* h_x, const lsq_opts& o, lsq_stats* stats);
+int group_iterate(Group& G, const double* const* h_b, int64_t iters, const lsq_opts& o, lsq_stats* stats);
+void referenced_cols(System& S, uint8_t* h_flags);
+void relabel_columns(System& S, const int32_t* h_map, int64_t n_local);
 
 // build.hip
 void form_from_coo(System& S, int64_t m, int64_t n_full, int64_t nnz, const int64_t* r,
                    const int64_t* c, const double* v);
 void finish_formation(System& S);              // G set -> GT, SELL copies, default scaling
-void refresh_scaling(System& S, int precond);   // rs/cs -> SELL values
+void refresh_scaling(System& S, int precond);   // rs/cs -> SELL values (single GPU)
+void scaling_rows_colnorm(System& S, int precond, bool raw);
+void scaling_finish_cs(System& S);
+void scaling_fill_values(System& S, int precond);
+bool scaling_stale(const System& S, int precond);
 void csr_spmv(System& S, int trans, const double* dx, double* dy);  // unweighted G / Gᵀ products
 
 // dense.hip

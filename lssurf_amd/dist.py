@@ -1,0 +1,309 @@
+"""Multi-GPU smooth_fit solve: y-slab partition of one least-squares system over ranks.
+
+SURVEY.md §8(e): every rank owns the unknowns (z0 and dz columns) of a band of node rows and
+the equations anchored there (stencil rows by their centre node, data rows by the point's y);
+stencils and the bilinear/trilinear interpolation reach one node row across a slab boundary,
+so a rank's rows touch one "ghost" node row per side.  The device solve then needs, per LSQR
+iteration, one forward halo (ghost ṽ before A·v), one reverse halo (ghost partial sums after
+Aᵀu) and two all-reduces of 1–2 doubles — liblsqsurf does those with RCCL over xGMI
+(``DistFitSystem``, one process per GPU) or, for testing on one GPU, between in-process
+virtual ranks (``VirtualDistFitSystem``).  Nothing here copies matrices between ranks: each
+rank's device generates its own rows from the shared grid/stencil description.
+"""
+import ctypes
+
+import numpy as np
+
+from . import assemble
+from ._native import LsqStats, NativeError, as_c, default_opts, load, ptr
+from .solver import LSQSolver
+
+
+class SlabPartition:
+    """Node-row bands of the dz grid (the bulk of the unknowns); every other grid's rows, the
+    stencil centres and the data points follow by their y coordinate."""
+
+    def __init__(self, grid, nranks):
+        ny = int(grid.shape[0])
+        if nranks > ny:
+            raise ValueError(f'{nranks} ranks for {ny} node rows')
+        cuts = [int(round(k * ny / nranks)) for k in range(1, nranks)]
+        self.bounds = np.array([grid.ctrs[0][0] + (c - 0.5) * grid.delta[0] for c in cuts])
+        self.nranks = nranks
+
+    def owner(self, y):
+        return np.searchsorted(self.bounds, y, side='right')
+
+    def rows_of(self, grid, rank):
+        """[a, b): the node rows of `grid` owned by `rank` (contiguous)."""
+        own = np.flatnonzero(self.owner(grid.ctrs[0]) == rank)
+        return (int(own[0]), int(own[-1]) + 1) if own.size else (0, 0)
+
+
+def rank_problem(G_data, Gc, partition, rank):
+    """Descriptors of the rows `rank` owns + their global row ids (None: not structured)."""
+    desc = assemble.describe(G_data, Gc)
+    if desc is None:
+        raise NotImplementedError('distributed solve needs a structured (stencil + interp) system')
+    grid_descs, interp, (py, px, pt), stencils, npts = desc
+    grid_objs = {}
+    for p in list(G_data.parts) + list(Gc.parts):
+        grid_objs[id(p['grid'])] = p['grid']
+    # the descriptor order of describe() is first-seen order over G_data then Gc parts
+    order, seen = [], set()
+    for p in list(G_data.parts) + list(Gc.parts):
+        if id(p['grid']) not in seen:
+            seen.add(id(p['grid']))
+            order.append(p['grid'])
+    pts_own = np.flatnonzero(partition.owner(py) == rank)
+    rows = [pts_own]
+    local = []
+    row0 = pts_own.size
+    for s, part in zip(stencils, Gc.parts):
+        g = order[s.grid]
+        a, b = partition.rows_of(g, rank)
+        lo_y, hi_y = max(int(s.lo[0]), a), min(int(s.hi[0]), b)
+        if lo_y >= hi_y:
+            continue
+        nd = int(g.N_dims)
+        inner = int(np.prod([int(s.hi[d]) - int(s.lo[d]) for d in range(1, nd)]))
+        t = type(s).from_buffer_copy(s)
+        t.lo[0], t.hi[0] = lo_y, hi_y
+        t.n_eq = (hi_y - lo_y) * inner
+        t.row0 = row0
+        first = npts + int(part['row0']) + (lo_y - int(s.lo[0])) * inner
+        rows.append(first + np.arange(t.n_eq))
+        row0 += t.n_eq
+        local.append(t)
+    coords = (py[pts_own].copy(), px[pts_own].copy(), None if pt is None else pt[pts_own].copy())
+    return dict(grids=grid_descs, grid_objs=order, interp=interp, coords=coords, stencils=local,
+                npts=int(pts_own.size), rows=np.concatenate(rows), m=int(row0))
+
+
+def column_owner(keep_cols, grid_objs, partition):
+    """Owner rank of every compact column (global full column -> its grid node row -> y)."""
+    full = np.asarray(keep_cols)
+    owner = np.empty(full.size, dtype=np.int32)
+    done = np.zeros(full.size, dtype=bool)
+    for g in grid_objs:
+        sel = (full >= g.col_0) & (full < g.col_0 + g.N_nodes)
+        iy = (full[sel] - g.col_0) // int(g.stride[0])
+        owner[sel] = partition.owner(g.ctrs[0][iy])
+        done |= sel
+    if not done.all():
+        raise ValueError('columns outside every grid')
+    return owner
+
+
+def local_layout(flags, owner, rank):
+    """col_local (compact -> local id), n_local, n_own, ghosts {peer: sorted compact ids}."""
+    owned = np.flatnonzero(owner == rank)
+    ghost = np.flatnonzero(flags.astype(bool) & (owner != rank))
+    ghosts = {}
+    pieces = [owned]
+    for p in np.unique(owner[ghost]):
+        ids = ghost[owner[ghost] == p]
+        ghosts[int(p)] = ids
+        pieces.append(ids)
+    order = np.concatenate(pieces)
+    col_local = np.full(owner.size, -1, dtype=np.int32)
+    col_local[order] = np.arange(order.size, dtype=np.int32)
+    return col_local, int(order.size), int(owned.size), ghosts, owned
+
+
+def exchange_plan(rank, col_local, ghosts_of):
+    """Per-peer send lists (owned local ids, in the peer's ghost order) and receive counts."""
+    mine = ghosts_of[rank]
+    peers = sorted(set(mine) | {p for p, g in enumerate(ghosts_of) if rank in g})
+    send_cnt, send_idx, recv_cnt = [], [], []
+    for p in peers:
+        want = ghosts_of[p].get(rank, np.zeros(0, dtype=np.int64))
+        send_cnt.append(want.size)
+        send_idx.append(col_local[want])
+        recv_cnt.append(mine.get(p, np.zeros(0)).size)
+    send_idx = np.concatenate(send_idx).astype(np.int32) if send_idx else np.zeros(0, np.int32)
+    return (np.array(peers, dtype=np.int32), np.array(send_cnt, dtype=np.int64), send_idx,
+            np.array(recv_cnt, dtype=np.int64))
+
+
+def _form_rank(L, h, prob, keep_cols, n_full):
+    from ._native import GridDesc, StencilDesc
+    s = _HandleView(L, h)
+    keep = as_c(keep_cols, np.int64)
+    s.check(L.lsq_set_col_map(h, int(n_full), ptr(keep), keep.size), 'lsq_set_col_map')
+    ga = (GridDesc * len(prob['grids']))(*prob['grids'])
+    sa = (StencilDesc * max(len(prob['stencils']), 1))(*prob['stencils'])
+    ig = as_c(np.asarray(prob['interp'], np.int32), np.int32)
+    py, px, pt = prob['coords']
+    s.check(L.lsq_set_matrix_stencil(h, prob['m'], int(n_full), len(prob['grids']), ctypes.cast(ga, ctypes.c_void_p),
+                                     len(prob['interp']), ptr(ig), prob['npts'], ptr(py), ptr(px), ptr(pt),
+                                     len(prob['stencils']), ctypes.cast(sa, ctypes.c_void_p), None),
+            'lsq_set_matrix_stencil')
+    flags = np.zeros(keep.size, np.uint8)
+    s.check(L.lsq_dist_referenced_cols(h, ptr(flags)), 'lsq_dist_referenced_cols')
+    return flags
+
+
+def _install_layout(L, h, lay, plan):
+    col_local, n_local, n_own = lay[:3]
+    peers, send_cnt, send_idx, recv_cnt = plan
+    _HandleView(L, h).check(
+        L.lsq_dist_set_layout(h, ptr(col_local), n_local, n_own, peers.size, ptr(peers), ptr(send_cnt), ptr(send_idx),
+                              ptr(recv_cnt)), 'lsq_dist_set_layout')
+
+
+class _HandleView:
+    def __init__(self, L, h):
+        self.L, self.h = L, h
+
+    def check(self, rc, what):
+        if rc < 0:
+            raise NativeError(f'{what}: {self.L.lsq_last_error(self.h).decode()}')
+        return rc
+
+
+class _Base:
+    def _setup_common(self, G_data, Gc, keep_cols, n_full, nranks):
+        dz = [g for g in (p['grid'] for p in Gc.parts) if g.N_dims == 3]
+        base_grid = dz[0] if dz else Gc.parts[0]['grid']
+        self.partition = SlabPartition(base_grid, nranks)
+        self.keep_cols = np.asarray(keep_cols)
+        self.n_full = int(n_full)
+        self.n_data = int(G_data.N_eq)
+
+
+class DistFitSystem(_Base):
+    """One rank of a multi-GPU solve (RCCL).  `pg` is a torch.distributed process group used only
+    for set-up (RCCL id broadcast, ghost lists); the solve itself never touches torch."""
+
+    def __init__(self, G_data, Gc, keep_cols, n_full, rank, nranks, device, pg=None):
+        import torch.distributed as tdist
+        self.L = load()
+        self._setup_common(G_data, Gc, keep_cols, n_full, nranks)
+        self.rank, self.nranks = rank, nranks
+        uid = np.zeros(128, np.uint8)
+        if rank == 0 and self.L.lsq_dist_unique_id(ptr(uid)) != 0:
+            raise NativeError('lsq_dist_unique_id failed')
+        box = [uid.tobytes()]
+        tdist.broadcast_object_list(box, src=0, group=pg)
+        uid = np.frombuffer(box[0], np.uint8).copy()
+        self.h = self.L.lsq_create_dist(int(device), int(rank), int(nranks), ptr(uid))
+        if not self.h:
+            raise NativeError('lsq_create_dist failed (RCCL communicator)')
+        self.prob = rank_problem(G_data, Gc, self.partition, rank)
+        flags = _form_rank(self.L, self.h, self.prob, keep_cols, n_full)
+        owner = column_owner(keep_cols, self.prob['grid_objs'], self.partition)
+        self.layout = local_layout(flags, owner, rank)
+        gathered = [None] * nranks
+        tdist.all_gather_object(gathered, self.layout[3], group=pg)
+        self.plan = exchange_plan(rank, self.layout[0], gathered)
+        _install_layout(self.L, self.h, self.layout, self.plan)
+        self.owned_cols = self.layout[4]
+        self.stats = None
+
+    def _b(self, row_weight, rhs):
+        self.set_row_weight(row_weight)
+        return as_c(np.asarray(rhs)[self.prob['rows']], np.float64)
+
+    def set_row_weight(self, w):
+        wl = as_c(np.asarray(w)[self.prob['rows']], np.float64)
+        _HandleView(self.L, self.h).check(self.L.lsq_set_row_weight(self.h, ptr(wl)), 'lsq_set_row_weight')
+
+    def solve(self, row_weight, rhs, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1):
+        b = self._b(row_weight, rhs)
+        x = np.zeros(self.layout[2])
+        o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond))
+        st = LsqStats()
+        _HandleView(self.L, self.h).check(self.L.lsq_solve(self.h, ptr(b), ptr(x), ctypes.byref(o), ctypes.byref(st)),
+                                          'lsq_solve')
+        self.stats = st.as_dict()
+        return x   # owned compact columns self.owned_cols
+
+    def iterate(self, row_weight, rhs, iters, precond=1):
+        b = self._b(row_weight, rhs)
+        o = default_opts(precond=int(precond))
+        st = LsqStats()
+        _HandleView(self.L, self.h).check(
+            self.L.lsq_iterate(self.h, ptr(b), int(iters), ctypes.byref(o), ctypes.byref(st)), 'lsq_iterate')
+        return st.as_dict()
+
+    def info(self):
+        o = np.zeros(6, np.int64)
+        self.L.lsq_sell_info(self.h, ptr(o))
+        return dict(zip(['m', 'n', 'nnz', 'sell_A', 'sell_AT', 'device_bytes'], o.tolist()))
+
+    def close(self):
+        if getattr(self, 'h', None):
+            self.L.lsq_destroy(self.h)
+            self.h = None
+
+
+class VirtualDistFitSystem(_Base):
+    """All ranks of the partition in this process on one GPU (liblsqsurf virtual group):
+    identical kernels, plans and exchange order as the RCCL path."""
+
+    def __init__(self, G_data, Gc, keep_cols, n_full, nranks, device=0):
+        self.L = load()
+        self._setup_common(G_data, Gc, keep_cols, n_full, nranks)
+        self.nranks = nranks
+        self.g = self.L.lsq_vgroup_create(int(device), int(nranks))
+        if not self.g:
+            raise NativeError('lsq_vgroup_create failed')
+        self.probs, self.layouts, flags_all = [], [], []
+        for r in range(nranks):
+            h = self.L.lsq_vgroup_rank(self.g, r)
+            prob = rank_problem(G_data, Gc, self.partition, r)
+            flags_all.append(_form_rank(self.L, h, prob, keep_cols, n_full))
+            self.probs.append(prob)
+        owner = column_owner(keep_cols, self.probs[0]['grid_objs'], self.partition)
+        self.layouts = [local_layout(flags_all[r], owner, r) for r in range(nranks)]
+        ghosts_of = [lay[3] for lay in self.layouts]
+        for r in range(nranks):
+            _install_layout(self.L, self.L.lsq_vgroup_rank(self.g, r), self.layouts[r],
+                            exchange_plan(r, self.layouts[r][0], ghosts_of))
+        self.stats = None
+
+    def _check(self, rc, what):
+        if rc < 0:
+            raise NativeError(f'{what}: {self.L.lsq_vgroup_last_error(self.g).decode()}')
+
+    def _bs(self, row_weight, rhs):
+        bs = []
+        for r, prob in enumerate(self.probs):
+            h = self.L.lsq_vgroup_rank(self.g, r)
+            wl = as_c(np.asarray(row_weight)[prob['rows']], np.float64)
+            _HandleView(self.L, h).check(self.L.lsq_set_row_weight(h, ptr(wl)), 'lsq_set_row_weight')
+            bs.append(as_c(np.asarray(rhs)[prob['rows']], np.float64))
+        return bs
+
+    def solve(self, row_weight, rhs, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1):
+        bs = self._bs(row_weight, rhs)
+        xs = [np.zeros(lay[2]) for lay in self.layouts]
+        bp = (ctypes.c_void_p * self.nranks)(*[b.ctypes.data for b in bs])
+        xp = (ctypes.c_void_p * self.nranks)(*[x.ctypes.data for x in xs])
+        o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond))
+        st = LsqStats()
+        self._check(self.L.lsq_vgroup_solve(self.g, bp, xp, ctypes.byref(o), ctypes.byref(st)), 'lsq_vgroup_solve')
+        self.stats = st.as_dict()
+        x = np.zeros(self.keep_cols.size)
+        for lay, xr in zip(self.layouts, xs):
+            x[lay[4]] = xr
+        return x   # compact columns (same space as LSQSolver.solve)
+
+    def iterate(self, row_weight, rhs, iters, precond=1):
+        bs = self._bs(row_weight, rhs)
+        bp = (ctypes.c_void_p * self.nranks)(*[b.ctypes.data for b in bs])
+        o = default_opts(precond=int(precond))
+        st = LsqStats()
+        self._check(self.L.lsq_vgroup_iterate(self.g, bp, int(iters), ctypes.byref(o), ctypes.byref(st)),
+                    'lsq_vgroup_iterate')
+        return st.as_dict()
+
+    def close(self):
+        if getattr(self, 'g', None):
+            self.L.lsq_vgroup_destroy(self.g)
+            self.g = None
+
+
+__all__ = ['SlabPartition', 'rank_problem', 'column_owner', 'local_layout', 'exchange_plan', 'DistFitSystem',
+           'VirtualDistFitSystem', 'LSQSolver']

@@ -1,0 +1,130 @@
+"""Host side of the multi-GPU path (lssurf_amd.dist): y-slab partition, per-rank row
+descriptors, column ownership, ghost layout and exchange plans.  CPU only; the world_size-2
+case runs the plan exchange over torch.distributed (gloo) exactly as DistFitSystem does."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import lssurf_amd as LS
+from lssurf_amd import dist, synthetic
+from lssurf_amd.constraint_functions import reference_epoch_keep_cols
+
+
+def _system(name='t64'):
+    D, kw = synthetic.points(name)
+    S = LS.smooth_fit(data=D, return_fit_objects=True, VERBOSE=False, **kw)
+    keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch'])
+    return S, keep
+
+
+def _host_csr(S, keep):
+    A = sp.vstack([S['G_data'].toCSR(), S['Gc'].toCSR()]).tocsr()[:, keep].tocsr()
+    A.eliminate_zeros()
+    return A
+
+
+def _flags(A, rows):
+    f = np.zeros(A.shape[1], np.uint8)
+    f[np.unique(A[rows].indices)] = 1
+    return f
+
+
+@pytest.mark.parametrize('nranks', [1, 2, 3, 5])
+def test_rows_partitioned_exactly_once(nranks):
+    S, keep = _system()
+    part = dist.SlabPartition(S['grids']['dz'], nranks)
+    m = S['G_data'].N_eq + S['Gc'].N_eq
+    probs = [dist.rank_problem(S['G_data'], S['Gc'], part, r) for r in range(nranks)]
+    allrows = np.concatenate([p['rows'] for p in probs])
+    np.testing.assert_array_equal(np.sort(allrows), np.arange(m))
+    for p in probs:
+        assert p['m'] == p['rows'].size
+        assert p['npts'] + sum(s.n_eq for s in p['stencils']) == p['m']
+        assert np.all(np.diff(p['rows'][:p['npts']]) > 0)
+
+
+@pytest.mark.parametrize('nranks', [2, 4])
+def test_ghosts_only_from_neighbouring_slabs(nranks):
+    S, keep = _system()
+    A = _host_csr(S, keep)
+    part = dist.SlabPartition(S['grids']['dz'], nranks)
+    probs = [dist.rank_problem(S['G_data'], S['Gc'], part, r) for r in range(nranks)]
+    owner = dist.column_owner(keep, probs[0]['grid_objs'], part)
+    assert np.bincount(owner, minlength=nranks).min() > 0
+    lays = [dist.local_layout(_flags(A, p['rows']), owner, r) for r, p in enumerate(probs)]
+    for r, lay in enumerate(lays):
+        col_local, n_local, n_own, ghosts, owned = lay
+        assert set(ghosts) <= {r - 1, r + 1}
+        assert n_own == owned.size and n_local == n_own + sum(g.size for g in ghosts.values())
+        np.testing.assert_array_equal(col_local[owned], np.arange(n_own))
+    # owned sets tile the columns; every column is referenced by some rank's rows
+    np.testing.assert_array_equal(np.sort(np.concatenate([l[4] for l in lays])), np.arange(keep.size))
+
+
+def test_exchange_plans_are_mirrored():
+    S, keep = _system()
+    A = _host_csr(S, keep)
+    nr = 3
+    part = dist.SlabPartition(S['grids']['dz'], nr)
+    probs = [dist.rank_problem(S['G_data'], S['Gc'], part, r) for r in range(nr)]
+    owner = dist.column_owner(keep, probs[0]['grid_objs'], part)
+    lays = [dist.local_layout(_flags(A, p['rows']), owner, r) for r, p in enumerate(probs)]
+    ghosts_of = [l[3] for l in lays]
+    plans = [dist.exchange_plan(r, lays[r][0], ghosts_of) for r in range(nr)]
+    _check_mirrored(lays, plans)
+
+
+def _check_mirrored(lays, plans):
+    nr = len(lays)
+    for r in range(nr):
+        peers, send_cnt, send_idx, recv_cnt = plans[r]
+        off = np.r_[0, np.cumsum(send_cnt)]
+        for k, p in enumerate(peers):
+            pk = list(plans[p][0]).index(r)
+            assert send_cnt[k] == plans[p][3][pk]          # what r sends is what p receives
+            owned_r = lays[r][4]
+            sent_global = owned_r[send_idx[off[k]:off[k + 1]]]
+            np.testing.assert_array_equal(sent_global, lays[p][3][r])   # in p's ghost-slot order
+
+
+def _worker(rank, world, port, outq):
+    import torch.distributed as tdist
+    tdist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank, world_size=world)
+    try:
+        S, keep = _system()
+        A = _host_csr(S, keep)
+        part = dist.SlabPartition(S['grids']['dz'], world)
+        prob = dist.rank_problem(S['G_data'], S['Gc'], part, rank)
+        owner = dist.column_owner(keep, prob['grid_objs'], part)
+        lay = dist.local_layout(_flags(A, prob['rows']), owner, rank)
+        gathered = [None] * world
+        tdist.all_gather_object(gathered, lay[3])
+        plan = dist.exchange_plan(rank, lay[0], gathered)
+        allp = [None] * world
+        tdist.all_gather_object(allp, (lay, plan))
+        if rank == 0:
+            _check_mirrored([a[0] for a in allp], [a[1] for a in allp])
+        outq.put((rank, 'ok'))
+    except Exception as e:   # report to the parent
+        outq.put((rank, repr(e)))
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_gloo_world2_plan_exchange():
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert res == {0: 'ok', 1: 'ok'}, res
