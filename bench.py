@@ -50,6 +50,52 @@ def build_system(config, device):
     return fs, rhs, w, {'host_assembly_s': t1 - t0, 'device_formation_s': t2 - t1}
 
 
+def build_dist_system(config, rank, world, device):
+    """One rank of the y-slab distributed system (lssurf_amd.dist): every rank assembles the
+    (lazy) operator description, generates only its own rows on its GPU and joins the RCCL
+    communicator."""
+    import lssurf_amd as LS
+    from lssurf_amd import synthetic
+    from lssurf_amd.constraint_functions import reference_epoch_keep_cols
+    from lssurf_amd.dist import DistFitSystem
+    t0 = time.time()
+    D, kw = synthetic.points(config)
+    S = LS.smooth_fit(data=D, return_fit_objects=True, VERBOSE=False, **kw)
+    keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch'])
+    t1 = time.time()
+    ds = DistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, rank, world, device)
+    E_all = 1 / (1. / np.concatenate((S['Ed'], S['Ec'])))
+    w = 1. / np.sqrt(E_all ** 2)
+    rhs = np.zeros(w.size)
+    rhs[:S['data'].size] = S['data'].z
+    ds.iterate(w, rhs, 1)       # uploads weights / local rhs, builds the scaling and workspace
+    t2 = time.time()
+    return ds, rhs, w, {'host_assembly_s': t1 - t0, 'device_formation_s': t2 - t1}
+
+
+class _Dist:
+    """bench adapter: the same calls on a DistFitSystem rank as on an LSQSolver."""
+
+    def __init__(self, ds):
+        self.ds = ds
+
+    def info(self):
+        return self.ds.info()
+
+    def iterate(self, rhs, iters):
+        return self.ds.iterate(None, None, iters)
+
+    def solve(self, rhs):
+        x = self.ds.solve(None, None)
+        return x, self.ds.stats
+
+    def profile_kernels(self, reps=10):
+        import ctypes
+        ms = np.zeros(4)
+        self.ds.L.lsq_profile_kernels(self.ds.h, int(reps), ms.ctypes.data_as(ctypes.c_void_p))
+        return dict(zip(['xw_spmv', 'spmtv', 'beta', 'givens'], ms.tolist()))
+
+
 def cpu_baseline(fs, b_weighted, sample_iters, threads):
     """oracle/lsqr_cpu.c on the same formed A (downloaded from the device) and the same
     weighted rhs; a bounded sample of iterations, timed on this host's cores."""
@@ -61,6 +107,58 @@ def cpu_baseline(fs, b_weighted, sample_iters, threads):
                                       f'OpenMP, column-scaled), {st["time_s"]:.1f} s'}
 
 
+KERNEL_SYMBOL = {'xw_spmv': 'k_xw_spmv', 'spmtv': 'k_spmtv'}
+
+
+def pmc_traffic(config, timeout=300):
+    """HBM-side bytes per launch of each iteration kernel from rocprofv3 PMC counters, collected in two
+    separate passes (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass on gfx950) of a short
+    child run of this script.  Units: KiB.  FETCH_SIZE is doubled: on gfx950 it reports exactly
+    half the bytes of coalesced 4/8/16-B-per-lane streams (MI355X_MICROARCH.md §HBM; our own
+    widths calibrated by profiles/calib_fetch.hip, profiles/r01_calib_fetch.md).  Counts
+    Infinity-Cache hits too (the counters sit on the L2's fabric side).  Returns None (+ reason)
+    when rocprofv3 is unavailable or fails.  Runs before this process touches the GPU."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    exe = shutil.which('rocprofv3')
+    if exe is None:
+        return None, 'rocprofv3 not found'
+    vals = {}
+    with tempfile.TemporaryDirectory(dir=os.environ.get('TMPDIR', '/tmp')) as tmp:
+        for ctr in ('FETCH_SIZE', 'WRITE_SIZE'):
+            out = os.path.join(tmp, ctr)
+            cmd = [exe, '--pmc', ctr, '-d', out, '-o', 'run', '--output-format', 'csv', '--',
+                   sys.executable, os.path.abspath(__file__), '--pmc-child', '--config', config]
+            try:
+                r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=timeout,
+                                   env=dict(os.environ, TMPDIR=tmp))
+            except subprocess.TimeoutExpired:
+                return None, f'rocprofv3 --pmc {ctr} timed out'
+            if r.returncode != 0:
+                return None, f'rocprofv3 --pmc {ctr} rc={r.returncode}'
+            files = [os.path.join(dp, f) for dp, _, fs in os.walk(out) for f in fs if f.endswith('counter_collection.csv')]
+            for kernel, sym in KERNEL_SYMBOL.items():
+                xs = []
+                for f in files:
+                    for row in csv.DictReader(open(f)):
+                        if sym + '(' in row['Kernel_Name'] and row['Counter_Name'] == ctr:
+                            xs.append(float(row['Counter_Value']))
+                if not xs:
+                    return None, f'no {ctr} samples for {kernel}'
+                vals[kernel, ctr] = sum(xs) / len(xs) * 1024.0
+    return {k: {'fetch_bytes': 2.0 * vals[k, 'FETCH_SIZE'], 'write_bytes': vals[k, 'WRITE_SIZE'],
+                'total': 2.0 * vals[k, 'FETCH_SIZE'] + vals[k, 'WRITE_SIZE']} for k in KERNEL_SYMBOL}, None
+
+
+def pmc_child(config):
+    """Short run under the profiler: formation + a few iterations of each kernel."""
+    fs, rhs, w, _ = build_system(config, 0)
+    fs.solver.iterate(rhs, 4)
+    fs.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -70,7 +168,15 @@ def main():
     ap.add_argument('--no-solve', action='store_true', help='skip the full solve to tolerance')
     ap.add_argument('--cpu-iters', type=int, default=10)
     ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--dist', action='store_true', help='use the distributed (RCCL) path even at N=1')
+    ap.add_argument('--no-pmc', action='store_true', help='skip the rocprofv3 PMC traffic passes')
+    ap.add_argument('--pmc-child', action='store_true', help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.pmc_child:
+        return pmc_child(args.config)
+    pmc, pmc_note = None, 'skipped (--no-pmc, --dist or N>1)'
+    if int(os.environ.get('WORLD_SIZE', '1')) == 1 and not args.no_pmc and not args.dist:
+        pmc, pmc_note = pmc_traffic(args.config)   # child processes, before this one touches the GPU
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -80,18 +186,24 @@ def main():
         import torch.distributed as dist
         dist.init_process_group('gloo', init_method='env://')
 
-    fs, rhs, w, setup = build_system(args.config, local)
-    info = fs.solver.info()
+    if world > 1 or args.dist:
+        ds, rhs, w, setup = build_dist_system(args.config, rank, world, local)
+        solver = _Dist(ds)
+        fs = ds
+    else:
+        fs, rhs, w, setup = build_system(args.config, local)
+        solver = fs.solver
+    info = solver.info()
     log(f'system: {info}, setup {setup}')
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    fs.solver.iterate(rhs, args.warmup)
+    solver.iterate(rhs, args.warmup)
     barrier()
     t0 = time.perf_counter()
-    st = fs.solver.iterate(rhs, args.steps)   # synchronous: returns after the device finished
+    st = solver.iterate(rhs, args.steps)   # synchronous: returns after the device finished
     barrier()
     t_wall = time.perf_counter() - t0
     t_dev = st['time_s']
@@ -102,11 +214,19 @@ def main():
         t_wall = float(tt[0])
 
     ms_per_step = 1e3 * t_wall / args.steps
-    value = world * args.steps / t_wall   # independent replicas
-    Z, m, n = info['nnz'], info['m'], info['n']
+    value = args.steps / t_wall   # LSQR iterations of the ONE (row-partitioned) system per second
+    Z, m, n = info['nnz'], info['m'], info['n']      # this rank's (local) system
+    gm, gZ, gn = m, Z, n
+    if dist is not None:                              # whole-system sizes for the config record
+        import torch
+        tt = torch.tensor([m, Z], dtype=torch.int64)
+        dist.all_reduce(tt)
+        gm, gZ = int(tt[0]), int(tt[1])
+    if isinstance(solver, _Dist):
+        gn = int(fs.keep_cols.size)
     bytes_iter = st['bytes_per_iter']
 
-    prof = fs.solver.profile_kernels(reps=10)
+    prof = solver.profile_kernels(reps=10)
     # algorithmic bytes per launch (DESIGN.md §Byte model)
     kb = {'spmtv': 12.0 * Z + 8.0 * m + 16.0 * n, 'xw_spmv': 12.0 * Z + 16.0 * m + 48.0 * n}
     dom = max(('spmtv', 'xw_spmv'), key=lambda k: prof[k])
@@ -114,29 +234,32 @@ def main():
 
     solve = {}
     if not args.no_solve:
-        x, sst = fs.solver.solve(rhs)
+        x, sst = solver.solve(rhs)
         solve = {'solve_time_s': sst['time_s'], 'solve_iters': int(sst['iters']), 'solve_istop': int(sst['istop'])}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and not args.dist:
         threads = min(os.cpu_count() or 1, 16)
         cpu = cpu_baseline(fs, w * rhs, args.cpu_iters, threads)
     fs.close()
+
+    traffic, traffic_note = (pmc[dom]['total'], pmc) if pmc else (None, pmc_note)
 
     if rank == 0:
         out = {
             'metric': 'LSQR iters/sec + solve wall-time, 1024x1024x12 grid / 2M pts, 1-8 GPU',
             'value': value, 'unit': 'LSQR iters/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': ms_per_step, 'higher_is_better': True,
-            'scaling': 'weak' if world > 1 else 'strong', 'vs_baseline': None, 'dtype': 'f64',
+            'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f64',
             'data': 'synthetic (SURVEY.md §8(d) point cloud)',
-            'config': {'workload': f'smooth_fit LSQR, {args.config}', 'grid': info, 'rows': m, 'cols': n,
-                       'nnz': Z, 'precond': 'column scaling', 'mode': 'replicas' if world > 1 else 'single'},
+            'config': {'workload': f'smooth_fit LSQR, {args.config}', 'rank0_system': info, 'rows': gm, 'cols': gn,
+                       'nnz': gZ, 'precond': 'column scaling',
+                       'parallelism': f'y-slab rows x{world} (RCCL)' if world > 1 or args.dist else 'single'},
             'device_iter_ms': 1e3 * t_dev / args.steps,
             'hbm_gbs_iter': bytes_iter * args.steps / t_dev / 1e9,
             'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
-                         'kernel_ms': prof},
+                         'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                         'algorithmic_bytes': kb[dom], 'traffic_detail': traffic_note, 'kernel_ms': prof},
             'cpu_baseline': cpu,
             **solve, **setup,
         }

@@ -223,6 +223,7 @@ void form_from_stencils(System& S, int64_t m, int64_t n_full, int32_t n_grids, c
     HIP_CHECK(hipStreamSynchronize(strm));
     if (herr) throw std::invalid_argument("lsq_set_matrix_stencil: " + std::to_string(herr) +
                                           " nonzero entries fall outside [0, n_full)");
+    S.n_sorted_rows = npts;   // data rows: point order is random in space
     finish_formation(S);
 }
 

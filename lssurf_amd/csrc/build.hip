@@ -11,6 +11,8 @@
 #include <algorithm>
 #include <vector>
 
+#include <hipcub/hipcub.hpp>
+
 #include "system.hpp"
 
 namespace lsq {
@@ -184,28 +186,64 @@ __global__ __launch_bounds__(BLOCK) void k_seg_sort(int64_t n, const int64_t* __
 }
 
 // ---- SELL-64 ---------------------------------------------------------------------------------
+// SELL row r holds CSR row perm[r] (perm may be null = identity); column ids may be remapped
+// through cmap (AT: A's CSR row ids -> A's SELL row ids).
 __global__ __launch_bounds__(BLOCK) void k_slice_width(int64_t rows, int64_t nslices,
                                                        const int64_t* __restrict__ rp,
+                                                       const int32_t* __restrict__ perm,
                                                        int64_t* __restrict__ wid) {
     for (int64_t s = (int64_t)blockIdx.x * BLOCK + threadIdx.x; s < nslices; s += (int64_t)gridDim.x * BLOCK) {
         int64_t w = 0;
         const int64_t r0 = s * SELL_C;
         const int64_t r1 = r0 + SELL_C < rows ? r0 + SELL_C : rows;
-        for (int64_t r = r0; r < r1; ++r) w = max(w, rp[r + 1] - rp[r]);
+        for (int64_t r = r0; r < r1; ++r) {
+            const int64_t q = perm ? perm[r] : r;
+            w = max(w, rp[q + 1] - rp[q]);
+        }
         wid[s] = w * SELL_C;
     }
 }
 
 __global__ __launch_bounds__(BLOCK) void k_sell_cols(int64_t rows, const int64_t* __restrict__ rp,
                                                      const int32_t* __restrict__ ci,
+                                                     const int32_t* __restrict__ perm,
+                                                     const int32_t* __restrict__ cmap,
                                                      const int64_t* __restrict__ sp, int32_t* __restrict__ sci) {
     for (int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BLOCK) {
         const int64_t s = r / SELL_C, lane = r % SELL_C;
+        const int64_t q = perm ? perm[r] : r;
         const int64_t base = sp[s], W = (sp[s + 1] - base) / SELL_C;
-        const int64_t b = rp[r], L = rp[r + 1] - b;
-        const int32_t padc = L ? ci[b + L - 1] : 0;
-        for (int64_t k = 0; k < W; ++k) sci[base + k * SELL_C + lane] = k < L ? ci[b + k] : padc;
+        const int64_t b = rp[q], L = rp[q + 1] - b;
+        for (int64_t k = 0; k < W; ++k) {
+            int32_t c = ci[b + (k < L ? k : L - 1)];
+            if (!L) c = 0;
+            sci[base + k * SELL_C + lane] = cmap && L ? cmap[c] : c;
+        }
     }
+}
+
+// Row order of A's SELL copy.  Rows are grouped by length (equal-length rows share slices: no
+// padding).  Within a length, the first `n_sorted` rows (the data rows: they arrive in point
+// order, which is random in space) are ordered by their first column, so the rows of a slice
+// gather from a few cache lines; the other rows (stencil rows, already in grid order) keep their
+// order, so each stencil part stays contiguous and Aᵀ's gathers of u stay coalesced.
+__global__ __launch_bounds__(BLOCK) void k_row_keys(int64_t m, int64_t n_sorted, const int64_t* __restrict__ rp,
+                                                    const int32_t* __restrict__ ci,
+                                                    unsigned long long* __restrict__ key,
+                                                    int32_t* __restrict__ id) {
+    for (int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x; r < m; r += (int64_t)gridDim.x * BLOCK) {
+        const int64_t L = rp[r + 1] - rp[r];
+        const bool by_col = r < n_sorted && L > 0;
+        const unsigned long long v = by_col ? (unsigned long long)(uint32_t)ci[rp[r]] : (unsigned long long)r;
+        key[r] = ((unsigned long long)L << 33) | ((unsigned long long)(by_col ? 0 : 1) << 32) | v;
+        id[r] = (int32_t)r;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_invert(int64_t m, const int32_t* __restrict__ perm,
+                                                  int32_t* __restrict__ inv) {
+    for (int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x; r < m; r += (int64_t)gridDim.x * BLOCK)
+        inv[perm[r]] = (int32_t)r;
 }
 
 // val_sell = (g * rs[row]) * cs[col]; `rowsc`/`colsc` index by the CSR's own row / column ids.
@@ -213,17 +251,19 @@ __global__ __launch_bounds__(BLOCK) void k_sell_vals(int64_t rows, const int64_t
                                                      const int32_t* __restrict__ ci, const double* __restrict__ g,
                                                      const double* __restrict__ rowsc,
                                                      const double* __restrict__ colsc, int transposed,
+                                                     const int32_t* __restrict__ perm,
                                                      const int64_t* __restrict__ sp, double* __restrict__ sval) {
     for (int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BLOCK) {
         const int64_t s = r / SELL_C, lane = r % SELL_C;
+        const int64_t q = perm ? perm[r] : r;   // CSR row
         const int64_t base = sp[s], W = (sp[s + 1] - base) / SELL_C;
-        const int64_t b = rp[r], L = rp[r + 1] - b;
+        const int64_t b = rp[q], L = rp[q + 1] - b;
         for (int64_t k = 0; k < W; ++k) {
             double x = 0.0;
             if (k < L) {
                 const int32_t c = ci[b + k];
-                // A: row scale of r, col scale of c.  AT: row scale of c, col scale of r.
-                x = transposed ? (g[b + k] * rowsc[c]) * colsc[r] : (g[b + k] * rowsc[r]) * colsc[c];
+                // A: row scale of q, col scale of c.  AT: row scale of c, col scale of q.
+                x = transposed ? (g[b + k] * rowsc[c]) * colsc[q] : (g[b + k] * rowsc[q]) * colsc[c];
             }
             sval[base + k * SELL_C + lane] = x;
         }
@@ -317,12 +357,14 @@ void check_err(BuildErr* d_err, hipStream_t s, const char* stage) {
     }
 }
 
-void build_sell(Sell& S, const Csr& C, hipStream_t st) {
+void build_sell(Sell& S, const Csr& C, const int32_t* cmap, hipStream_t st) {
     S.rows = C.m;
     S.nslices = (C.m + SELL_C - 1) / SELL_C;
     S.sp.alloc(S.nslices + 1);
     S.sp.zero(st);
-    hipLaunchKernelGGL(k_slice_width, dim3(grid_for(S.nslices)), dim3(BLOCK), 0, st, C.m, S.nslices, C.rp.p, S.sp.p);
+    const int32_t* perm = S.perm.n ? S.perm.p : nullptr;
+    hipLaunchKernelGGL(k_slice_width, dim3(grid_for(S.nslices)), dim3(BLOCK), 0, st, C.m, S.nslices, C.rp.p, perm,
+                       S.sp.p);
     KERNEL_CHECK();
     S.nent = exclusive_scan_i64(S.sp.p, S.nslices + 1, st);
     S.ci.alloc(std::max<int64_t>(S.nent, 1));
@@ -331,8 +373,29 @@ void build_sell(Sell& S, const Csr& C, hipStream_t st) {
     // give them column 0 and value 0 so any read of them is in bounds and contributes nothing
     S.ci.zero(st);
     S.val.zero(st);
-    hipLaunchKernelGGL(k_sell_cols, dim3(grid_for(C.m)), dim3(BLOCK), 0, st, C.m, C.rp.p, C.ci.p, S.sp.p, S.ci.p);
+    hipLaunchKernelGGL(k_sell_cols, dim3(grid_for(C.m)), dim3(BLOCK), 0, st, C.m, C.rp.p, C.ci.p, perm, cmap, S.sp.p,
+                       S.ci.p);
     KERNEL_CHECK();
+}
+
+// A's SELL row order (k_row_keys): one radix sort of 64-bit keys.
+void locality_order(const Csr& G, int64_t n_sorted, DBuf<int32_t>& perm, DBuf<int32_t>& inv, hipStream_t st) {
+    const int64_t m = G.m;
+    perm.alloc(std::max<int64_t>(m, 1));
+    inv.alloc(std::max<int64_t>(m, 1));
+    if (m == 0) return;
+    if (m >= (int64_t(1) << 31)) throw std::invalid_argument("more than 2^31 rows");
+    DBuf<unsigned long long> k0(m), k1(m);
+    DBuf<int32_t> id(m);
+    hipLaunchKernelGGL(k_row_keys, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, n_sorted, G.rp.p, G.ci.p, k0.p, id.p);
+    KERNEL_CHECK();
+    size_t tmp_bytes = 0;
+    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, k0.p, k1.p, id.p, perm.p, (int)m, 0, 64, st));
+    DBuf<unsigned char> tmp((int64_t)tmp_bytes + 1);
+    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tmp_bytes, k0.p, k1.p, id.p, perm.p, (int)m, 0, 64, st));
+    hipLaunchKernelGGL(k_invert, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, perm.p, inv.p);
+    KERNEL_CHECK();
+    HIP_CHECK(hipStreamSynchronize(st));
 }
 
 }  // namespace
@@ -389,6 +452,7 @@ void form_from_coo(System& S, int64_t m, int64_t n_full, int64_t nnz, const int6
     tc.release();
     tv.release();
     off.release();
+    S.n_sorted_rows = 0;
     finish_formation(S);
 }
 
@@ -422,8 +486,10 @@ void finish_formation(System& S) {
     KERNEL_CHECK();
     check_err(err.p, st, "lsq_set_matrix_coo (transpose)");
 
-    build_sell(S.A, G, st);
-    build_sell(S.AT, T, st);
+    DBuf<int32_t> inv;
+    locality_order(G, S.n_sorted_rows, S.A.perm, inv, st);
+    build_sell(S.A, G, nullptr, st);
+    build_sell(S.AT, T, inv.p, st);   // AT's column ids = A's SELL row ids
 
     // default scaling state: weights 1, all rows kept, no preconditioner
     S.roww.alloc(m);
@@ -465,10 +531,10 @@ void scaling_fill_values(System& S, int precond) {
     hipStream_t st = S.stream;
     const int64_t m = S.G.m, n = S.G.n;
     hipLaunchKernelGGL(k_sell_vals, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, S.G.rp.p, S.G.ci.p, S.G.val.p, S.rs.p,
-                       S.cs.p, 0, S.A.sp.p, S.A.val.p);
+                       S.cs.p, 0, S.A.perm.p, S.A.sp.p, S.A.val.p);
     KERNEL_CHECK();
     hipLaunchKernelGGL(k_sell_vals, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, S.GT.rp.p, S.GT.ci.p, S.GT.val.p, S.rs.p,
-                       S.cs.p, 1, S.AT.sp.p, S.AT.val.p);
+                       S.cs.p, 1, nullptr, S.AT.sp.p, S.AT.val.p);
     KERNEL_CHECK();
     S.rs_dirty = false;
     S.cs_mode = precond;

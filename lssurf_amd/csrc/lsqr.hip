@@ -58,8 +58,9 @@ __device__ __forceinline__ void store_partial(double acc, double* part, int slot
 __global__ __launch_bounds__(BLOCK) void k_init_u(int64_t m, int64_t nslices, const int64_t* __restrict__ sp,
                                                   const int32_t* __restrict__ ci, const double* __restrict__ val,
                                                   const double* __restrict__ rs, const double* __restrict__ b,
-                                                  const double* __restrict__ y0, double* __restrict__ u,
-                                                  double* __restrict__ bw, double* part_u, double* part_b) {
+                                                  const double* __restrict__ y0, const int32_t* __restrict__ perm,
+                                                  double* __restrict__ u, double* __restrict__ bw, double* part_u,
+                                                  double* part_b) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     double su = 0.0, sb = 0.0;
     for (int64_t s = (int64_t)blockIdx.x * 4 + wid; s < nslices; s += (int64_t)gridDim.x * 4) {
@@ -70,7 +71,8 @@ __global__ __launch_bounds__(BLOCK) void k_init_u(int64_t m, int64_t nslices, co
             ax = sell_row_dot(ci, val, base, (sp[s + 1] - base) / SELL_C, lane, y0);
         }
         if (row < m) {
-            const double bb = rs[row] * b[row];
+            const int64_t q = perm[row];   // u lives in A's SELL row order; b, rs in CSR order
+            const double bb = rs[q] * b[q];
             const double uu = bb - ax;
             bw[row] = bb;
             u[row] = uu;
@@ -466,7 +468,7 @@ void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts&
     // the SpMV of the warm start gathers in A·M coordinates: y0 for precond 0/1, x0 for precond 2
     const double* gather0 = h_x0 ? (dense ? dx0.p : dy0.p) : nullptr;
     hipLaunchKernelGGL(k_init_u, dim3(g.gA), dim3(BLOCK), 0, st, m, S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p,
-                       S.rs.p, db.p, gather0, S.u.p, S.bw.p, S.part_u.p, S.part_b.p);
+                       S.rs.p, db.p, gather0, S.A.perm.p, S.u.p, S.bw.p, S.part_u.p, S.part_b.p);
     KERNEL_CHECK();
     hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gA, S.part_b.p, g.gA, 1, nullptr);
     KERNEL_CHECK();

@@ -33,6 +33,7 @@ struct Sell {
     DBuf<int64_t> sp;   // nslices+1 entry offsets (multiples of 64)
     DBuf<int32_t> ci;   // nent
     DBuf<double> val;   // nent (padding: val 0, col = a valid column of the row)
+    DBuf<int32_t> perm; // SELL row -> CSR row (A only; empty = identity).  See build_sell.
 };
 
 // LSQR scalar state, device resident (one per handle).  Field meanings follow
@@ -60,6 +61,7 @@ struct System {
     // column map (Ip_c)
     int64_t n_full = 0, n_keep = 0;
     bool have_colmap = false;
+    int64_t n_sorted_rows = 0;   // leading rows ordered by first column in A's SELL copy (data rows)
     DBuf<int32_t> colmap;   // n_full -> compact index or -1
 
     Csr G, GT;

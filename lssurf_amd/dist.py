@@ -162,6 +162,21 @@ class _HandleView:
         return rc
 
 
+def _quiet_stdout(fn):
+    """RCCL prints a version banner on stdout at communicator creation; send it to stderr so a
+    rank's stdout stays machine-readable (bench.py prints exactly one JSON line)."""
+    import os
+    import sys
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        return fn()
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 class _Base:
     def _setup_common(self, G_data, Gc, keep_cols, n_full, nranks):
         dz = [g for g in (p['grid'] for p in Gc.parts) if g.N_dims == 3]
@@ -177,33 +192,41 @@ class DistFitSystem(_Base):
     for set-up (RCCL id broadcast, ghost lists); the solve itself never touches torch."""
 
     def __init__(self, G_data, Gc, keep_cols, n_full, rank, nranks, device, pg=None):
-        import torch.distributed as tdist
+        if nranks > 1:
+            import torch.distributed as tdist
         self.L = load()
         self._setup_common(G_data, Gc, keep_cols, n_full, nranks)
         self.rank, self.nranks = rank, nranks
         uid = np.zeros(128, np.uint8)
         if rank == 0 and self.L.lsq_dist_unique_id(ptr(uid)) != 0:
             raise NativeError('lsq_dist_unique_id failed')
-        box = [uid.tobytes()]
-        tdist.broadcast_object_list(box, src=0, group=pg)
-        uid = np.frombuffer(box[0], np.uint8).copy()
-        self.h = self.L.lsq_create_dist(int(device), int(rank), int(nranks), ptr(uid))
+        if nranks > 1:
+            box = [uid.tobytes()]
+            tdist.broadcast_object_list(box, src=0, group=pg)
+            uid = np.frombuffer(box[0], np.uint8).copy()
+        self.h = _quiet_stdout(lambda: self.L.lsq_create_dist(int(device), int(rank), int(nranks), ptr(uid)))
         if not self.h:
             raise NativeError('lsq_create_dist failed (RCCL communicator)')
         self.prob = rank_problem(G_data, Gc, self.partition, rank)
         flags = _form_rank(self.L, self.h, self.prob, keep_cols, n_full)
         owner = column_owner(keep_cols, self.prob['grid_objs'], self.partition)
         self.layout = local_layout(flags, owner, rank)
-        gathered = [None] * nranks
-        tdist.all_gather_object(gathered, self.layout[3], group=pg)
+        gathered = [self.layout[3]]
+        if nranks > 1:
+            gathered = [None] * nranks
+            tdist.all_gather_object(gathered, self.layout[3], group=pg)
         self.plan = exchange_plan(rank, self.layout[0], gathered)
         _install_layout(self.L, self.h, self.layout, self.plan)
         self.owned_cols = self.layout[4]
         self.stats = None
 
     def _b(self, row_weight, rhs):
-        self.set_row_weight(row_weight)
-        return as_c(np.asarray(rhs)[self.prob['rows']], np.float64)
+        """None keeps the weights / local rhs of the previous call (no host slicing)."""
+        if row_weight is not None:
+            self.set_row_weight(row_weight)
+        if rhs is not None:
+            self._b_local = as_c(np.asarray(rhs)[self.prob['rows']], np.float64)
+        return self._b_local
 
     def set_row_weight(self, w):
         wl = as_c(np.asarray(w)[self.prob['rows']], np.float64)
@@ -268,13 +291,14 @@ class VirtualDistFitSystem(_Base):
             raise NativeError(f'{what}: {self.L.lsq_vgroup_last_error(self.g).decode()}')
 
     def _bs(self, row_weight, rhs):
-        bs = []
-        for r, prob in enumerate(self.probs):
-            h = self.L.lsq_vgroup_rank(self.g, r)
-            wl = as_c(np.asarray(row_weight)[prob['rows']], np.float64)
-            _HandleView(self.L, h).check(self.L.lsq_set_row_weight(h, ptr(wl)), 'lsq_set_row_weight')
-            bs.append(as_c(np.asarray(rhs)[prob['rows']], np.float64))
-        return bs
+        if row_weight is not None:
+            for r, prob in enumerate(self.probs):
+                h = self.L.lsq_vgroup_rank(self.g, r)
+                wl = as_c(np.asarray(row_weight)[prob['rows']], np.float64)
+                _HandleView(self.L, h).check(self.L.lsq_set_row_weight(h, ptr(wl)), 'lsq_set_row_weight')
+        if rhs is not None:
+            self._b_local = [as_c(np.asarray(rhs)[prob['rows']], np.float64) for prob in self.probs]
+        return self._b_local
 
     def solve(self, row_weight, rhs, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1):
         bs = self._bs(row_weight, rhs)
