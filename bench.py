@@ -82,18 +82,20 @@ class _Dist:
     def info(self):
         return self.ds.info()
 
-    def iterate(self, rhs, iters):
+    def iterate(self, rhs, iters, op=0):
         return self.ds.iterate(None, None, iters)
 
-    def solve(self, rhs):
+    def solve(self, rhs, op=0):
         x = self.ds.solve(None, None)
         return x, self.ds.stats
 
-    def profile_kernels(self, reps=10):
+    def profile_kernels(self, reps=10, op=0):
         import ctypes
-        ms = np.zeros(4)
-        self.ds.L.lsq_profile_kernels(self.ds.h, int(reps), ms.ctypes.data_as(ctypes.c_void_p))
-        return dict(zip(['xw_spmv', 'spmtv', 'beta', 'givens'], ms.tolist()))
+        o = np.zeros(8)
+        self.ds.L.lsq_profile_kernels(self.ds.h, int(reps), 0, o.ctypes.data_as(ctypes.c_void_p))
+        d = dict(zip(['xw_spmv', 'spmtv', 'beta', 'givens'], o[:4].tolist()))
+        d['bytes'] = {'xw_spmv': float(o[4]), 'spmtv': float(o[5])}
+        return d
 
 
 def cpu_baseline(fs, b_weighted, sample_iters, threads):
@@ -107,10 +109,11 @@ def cpu_baseline(fs, b_weighted, sample_iters, threads):
                                       f'OpenMP, column-scaled), {st["time_s"]:.1f} s'}
 
 
-KERNEL_SYMBOL = {'xw_spmv': 'k_xw_spmv', 'spmtv': 'k_spmtv'}
+# kernel symbols per role: assembled-SELL operator / structured stencil operator
+KERNEL_SYMBOL = {'xw_spmv': ('k_xw_spmv(', 'k_mf_fwd('), 'spmtv': ('k_spmtv(', 'k_mf_spmtv(')}
 
 
-def pmc_traffic(config, timeout=300):
+def pmc_traffic(config, op, timeout=300):
     """HBM-side bytes per launch of each iteration kernel from rocprofv3 PMC counters, collected in two
     separate passes (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass on gfx950) of a short
     child run of this script.  Units: KiB.  FETCH_SIZE is doubled: on gfx950 it reports exactly
@@ -130,7 +133,7 @@ def pmc_traffic(config, timeout=300):
         for ctr in ('FETCH_SIZE', 'WRITE_SIZE'):
             out = os.path.join(tmp, ctr)
             cmd = [exe, '--pmc', ctr, '-d', out, '-o', 'run', '--output-format', 'csv', '--',
-                   sys.executable, os.path.abspath(__file__), '--pmc-child', '--config', config]
+                   sys.executable, os.path.abspath(__file__), '--pmc-child', '--config', config, '--op', str(op)]
             try:
                 r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=timeout,
                                    env=dict(os.environ, TMPDIR=tmp))
@@ -139,11 +142,11 @@ def pmc_traffic(config, timeout=300):
             if r.returncode != 0:
                 return None, f'rocprofv3 --pmc {ctr} rc={r.returncode}'
             files = [os.path.join(dp, f) for dp, _, fs in os.walk(out) for f in fs if f.endswith('counter_collection.csv')]
-            for kernel, sym in KERNEL_SYMBOL.items():
+            for kernel, syms in KERNEL_SYMBOL.items():
                 xs = []
                 for f in files:
                     for row in csv.DictReader(open(f)):
-                        if sym + '(' in row['Kernel_Name'] and row['Counter_Name'] == ctr:
+                        if any(x in row['Kernel_Name'] for x in syms) and row['Counter_Name'] == ctr:
                             xs.append(float(row['Counter_Value']))
                 if not xs:
                     return None, f'no {ctr} samples for {kernel}'
@@ -152,10 +155,10 @@ def pmc_traffic(config, timeout=300):
                 'total': 2.0 * vals[k, 'FETCH_SIZE'] + vals[k, 'WRITE_SIZE']} for k in KERNEL_SYMBOL}, None
 
 
-def pmc_child(config):
+def pmc_child(config, op):
     """Short run under the profiler: formation + a few iterations of each kernel."""
     fs, rhs, w, _ = build_system(config, 0)
-    fs.solver.iterate(rhs, 4)
+    fs.solver.iterate(rhs, 4, op=op)
     fs.close()
 
 
@@ -170,13 +173,14 @@ def main():
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--dist', action='store_true', help='use the distributed (RCCL) path even at N=1')
     ap.add_argument('--no-pmc', action='store_true', help='skip the rocprofv3 PMC traffic passes')
+    ap.add_argument('--op', type=int, default=0, help='0: auto (structured stencil operator), 1: assembled SELL')
     ap.add_argument('--pmc-child', action='store_true', help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
-        return pmc_child(args.config)
+        return pmc_child(args.config, args.op)
     pmc, pmc_note = None, 'skipped (--no-pmc, --dist or N>1)'
     if int(os.environ.get('WORLD_SIZE', '1')) == 1 and not args.no_pmc and not args.dist:
-        pmc, pmc_note = pmc_traffic(args.config)   # child processes, before this one touches the GPU
+        pmc, pmc_note = pmc_traffic(args.config, args.op)   # child processes, before this one touches the GPU
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -200,10 +204,10 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    solver.iterate(rhs, args.warmup)
+    solver.iterate(rhs, args.warmup, op=args.op)
     barrier()
     t0 = time.perf_counter()
-    st = solver.iterate(rhs, args.steps)   # synchronous: returns after the device finished
+    st = solver.iterate(rhs, args.steps, op=args.op)   # synchronous: returns after the device finished
     barrier()
     t_wall = time.perf_counter() - t0
     t_dev = st['time_s']
@@ -226,15 +230,15 @@ def main():
         gn = int(fs.keep_cols.size)
     bytes_iter = st['bytes_per_iter']
 
-    prof = solver.profile_kernels(reps=10)
+    prof = solver.profile_kernels(reps=10, op=args.op)
     # algorithmic bytes per launch (DESIGN.md §Byte model)
-    kb = {'spmtv': 12.0 * Z + 8.0 * m + 16.0 * n, 'xw_spmv': 12.0 * Z + 16.0 * m + 48.0 * n}
+    kb = prof.pop('bytes')   # algorithmic bytes per launch, from the library's byte model
     dom = max(('spmtv', 'xw_spmv'), key=lambda k: prof[k])
     achieved = kb[dom] / (prof[dom] * 1e-3) / 1e9
 
     solve = {}
     if not args.no_solve:
-        x, sst = solver.solve(rhs)
+        x, sst = solver.solve(rhs, op=args.op)
         solve = {'solve_time_s': sst['time_s'], 'solve_iters': int(sst['iters']), 'solve_istop': int(sst['istop'])}
 
     cpu = None
@@ -254,6 +258,8 @@ def main():
             'data': 'synthetic (SURVEY.md §8(d) point cloud)',
             'config': {'workload': f'smooth_fit LSQR, {args.config}', 'rank0_system': info, 'rows': gm, 'cols': gn,
                        'nnz': gZ, 'precond': 'column scaling',
+                       'operator': 'structured stencil rows + SELL data rows' if info.get('stencil_op') and args.op == 0
+                       and not isinstance(solver, _Dist) else 'assembled SELL',
                        'parallelism': f'y-slab rows x{world} (RCCL)' if world > 1 or args.dist else 'single'},
             'device_iter_ms': 1e3 * t_dev / args.steps,
             'hbm_gbs_iter': bytes_iter * args.steps / t_dev / 1e9,

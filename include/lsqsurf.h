@@ -50,7 +50,9 @@ typedef struct lsq_opts {
     int32_t use_x0;        /* 1: x_inout holds a warm start (outer-iteration "resume")          */
     int32_t batch;         /* iterations per device batch between host convergence checks      */
     int32_t use_graph;     /* 1: replay each batch as a captured hipGraph                       */
-    int32_t reserved;
+    int32_t op;            /* operator the iteration streams: 0 = auto (the structured stencil  */
+                           /*     operator when the matrix came from lsq_set_matrix_stencil and */
+                           /*     precond < 2; else assembled SELL), 1 = assembled SELL always  */
 } lsq_opts;
 
 /* Statistics (mirrors scipy's lsqr return tuple, plus timing and the byte model). */
@@ -176,12 +178,14 @@ int lsq_vgroup_iterate(lsq_vgroup* g, const double* const* b, int64_t iters, con
 const char* lsq_vgroup_last_error(lsq_vgroup* g);
 void lsq_vgroup_destroy(lsq_vgroup* g);
 
-/* Bench / profiling hooks.  lsq_profile_kernels times each iteration kernel in isolation
- * (reps launches each, HIP events on the handle's stream): ms4 = {x/w+SpMV, SpMTV, beta reduce,
- * rotation}.  It clobbers the iteration state.  lsq_sell_info: {m, n, nnz, SELL entries of A,
- * SELL entries of Aᵀ, device bytes of the operator copies}. */
-int lsq_profile_kernels(lsq_handle* h, int32_t reps, double* ms4);
-int lsq_sell_info(lsq_handle* h, int64_t* out6);
+/* Bench / profiling hooks.  lsq_profile_kernels times each iteration kernel of the operator
+ * `op` (lsq_opts.op) in isolation (reps launches each, HIP events on the handle's stream):
+ * out8 = {ms of x/w+A·v, ms of Aᵀu, ms of beta reduce, ms of rotation, algorithmic HBM bytes
+ * per launch of x/w+A·v, of Aᵀu (DESIGN.md §Byte model), 0, 0}.  It clobbers the iteration
+ * state.  lsq_sell_info: out8 = {m, n, nnz, SELL entries streamed by A·v, by Aᵀu, device bytes
+ * of the operator copies, 1 if the structured stencil operator is available, n_full}. */
+int lsq_profile_kernels(lsq_handle* h, int32_t reps, int32_t op, double* out8);
+int lsq_sell_info(lsq_handle* h, int64_t* out8);
 
 /* ---- triangular kernels (replace the Cython kernels; R upper triangular CSR, int32 indices,
  *      sorted column indices, diagonal first in each row) ------------------------------------ */

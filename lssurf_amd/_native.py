@@ -17,7 +17,7 @@ class LsqOpts(ctypes.Structure):
     _fields_ = [('method', ctypes.c_int32), ('precond', ctypes.c_int32), ('atol', ctypes.c_double),
                 ('btol', ctypes.c_double), ('conlim', ctypes.c_double), ('maxit', ctypes.c_int64),
                 ('use_x0', ctypes.c_int32), ('batch', ctypes.c_int32), ('use_graph', ctypes.c_int32),
-                ('reserved', ctypes.c_int32)]
+                ('op', ctypes.c_int32)]
 
 
 class GridDesc(ctypes.Structure):
@@ -77,7 +77,7 @@ def load():
         'lsq_solve': ([P, P, P, P, P], ctypes.c_int),
         'lsq_spmv': ([P, i32, P, P], ctypes.c_int),
         'lsq_iterate': ([P, P, i64, P, P], ctypes.c_int),
-        'lsq_profile_kernels': ([P, i32, P], ctypes.c_int),
+        'lsq_profile_kernels': ([P, i32, i32, P], ctypes.c_int),
         'lsq_sell_info': ([P, P], ctypes.c_int),
         'lsq_sigma_x': ([P, P], ctypes.c_int),
         'lsq_get_rinv': ([P, P], ctypes.c_int),

@@ -35,7 +35,7 @@ def _deps_newer(target, deps):
 
 def build(force=False, verbose=False):
     os.makedirs(OBJ, exist_ok=True)
-    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.hpp')]
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(('.hpp', '.inc'))]
     headers.append(os.path.join(os.path.dirname(HERE), 'include', 'lsqsurf.h'))
     jobs = []
     for src in SOURCES:

@@ -7,10 +7,9 @@
 #include "system.hpp"
 
 namespace lsq {
-void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts& o, bool no_stop);
 int lsqr_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq_stats* stats);
 int lsqr_iterate(System& S, const double* h_b, int64_t iters, const lsq_opts& o, lsq_stats* stats);
-void lsqr_profile(System& S, int reps, double* ms_out);
+void lsqr_profile(System& S, int reps, int op, double* out);
 void lsqr_sigma_x(System& S, double* h_E);
 void lsqr_get_rinv(System& S, double* h_Ri);
 void graph_cache_drop(const System* S);
@@ -267,23 +266,32 @@ int lsq_iterate(lsq_handle* h, const double* b, int64_t iters, const lsq_opts* o
     });
 }
 
-int lsq_profile_kernels(lsq_handle* h, int32_t reps, double* ms4) {
+int lsq_profile_kernels(lsq_handle* h, int32_t reps, int32_t op, double* out8) {
     return guarded(h, [&](lsq::System& S) {
         if (!S.G.rp.p) return fail(S, "lsq_profile_kernels: no matrix");
-        lsq::lsqr_profile(S, reps > 0 ? reps : 10, ms4);
+        if (!out8) return fail(S, "lsq_profile_kernels: null output");
+        lsq::graph_cache_drop(&S);
+        lsq::lsqr_profile(S, reps > 0 ? reps : 10, op, out8);
         return 0;
     });
 }
 
-int lsq_sell_info(lsq_handle* h, int64_t* out6) {
+int lsq_sell_info(lsq_handle* h, int64_t* out8) {
     return guarded(h, [&](lsq::System& S) {
-        out6[0] = S.G.m;
-        out6[1] = S.G.n;
-        out6[2] = S.G.nnz;
-        out6[3] = S.A.nent;
-        out6[4] = S.AT.nent;
-        out6[5] = (int64_t)(S.G.rp.bytes() + S.G.ci.bytes() + S.G.val.bytes() + S.GT.rp.bytes() + S.GT.ci.bytes() +
-                            S.GT.val.bytes() + S.A.ci.bytes() + S.A.val.bytes() + S.AT.ci.bytes() + S.AT.val.bytes());
+        if (!out8) return fail(S, "lsq_sell_info: null output");
+        out8[0] = S.G.m;
+        out8[1] = S.G.n;
+        out8[2] = S.G.nnz;
+        const lsq::Sell& a = S.mf ? S.Ad : S.A;
+        const lsq::Sell& t = S.mf ? S.ATd : S.AT;
+        out8[3] = a.nent;
+        out8[4] = t.nent;
+        out8[5] = (int64_t)(S.G.rp.bytes() + S.G.ci.bytes() + S.G.val.bytes() + S.GT.rp.bytes() + S.GT.ci.bytes() +
+                            S.GT.val.bytes() + S.A.ci.bytes() + S.A.val.bytes() + S.AT.ci.bytes() + S.AT.val.bytes() +
+                            S.Ad.ci.bytes() + S.Ad.val.bytes() + S.ATd.ci.bytes() + S.ATd.val.bytes() +
+                            S.GdT.ci.bytes() + S.GdT.val.bytes());
+        out8[6] = S.mf ? 1 : 0;
+        out8[7] = S.n_full;
         return 0;
     });
 }

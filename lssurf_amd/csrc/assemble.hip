@@ -142,6 +142,114 @@ __global__ __launch_bounds__(BLOCK) void k_gen_rows(int pass, const GenCtx* __re
     }
 }
 
+FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f{};
+    f.d = d;
+    uint32_t s = 0;
+    while ((uint64_t(1) << s) < d) ++s;
+    f.shift = s;
+    f.mul = (uint64_t)(((unsigned __int128)1 << (32 + s)) + d - 1) / d;   // ceil(2^(32+s) / d)
+    return f;
+}
+
+// The structured stencil operator (system.hpp MfDesc) when every part is a clean stencil:
+// every template entry of every centre in the box stays inside its grid, grids do not overlap,
+// and every index fits 31 bits.
+bool describe_stencil_operator(MfDesc& d, int64_t m, int64_t n_full, int32_t n_grids, const lsq_grid_desc* grids,
+                               int64_t npts, int32_t n_stencil, const lsq_stencil_desc* st) {
+    d = MfDesc{};
+    d.npts = npts;
+    d.m = m;
+    d.n_full = n_full;
+    if (n_grids > MF_MAX_GRIDS || m >= (int64_t(1) << 31) || n_full >= (int64_t(1) << 31)) return false;
+    for (int g = 0; g < n_grids; ++g) {
+        MfGrid& G = d.g[g];
+        G.ndim = 3;   // every grid is padded to 3 dims with trailing extent-1 dims (same ravel)
+        G.col0 = (int32_t)grids[g].col0;
+        int64_t s = 1;
+        for (int k = 2; k >= 0; --k) {
+            G.shape[k] = k < grids[g].ndim ? (int32_t)grids[g].shape[k] : 1;
+            G.fd[k] = make_fastdiv((uint32_t)std::max<int32_t>(G.shape[k], 1));
+            s *= G.shape[k];
+        }
+        G.nodes = (int32_t)s;
+        if (grids[g].col0 < 0 || grids[g].col0 + s > n_full) return false;
+        for (int h = 0; h < g; ++h)
+            if (G.col0 < d.g[h].col0 + d.g[h].nodes && d.g[h].col0 < G.col0 + s) return false;
+    }
+    d.n_grids = n_grids;
+    for (int i = 0; i < n_stencil; ++i) {
+        const lsq_stencil_desc& S = st[i];
+        if (S.n_eq == 0) continue;
+        if (d.n_parts == MF_MAX_PARTS) return false;
+        MfGrid& G = d.g[S.grid];
+        if (G.nparts == MF_MAX_GRID_PARTS) return false;
+        MfPart& P = d.p[d.n_parts];
+        P.grid = S.grid;
+        P.ntpl = S.ntpl;
+        P.row0 = (int32_t)S.row0;
+        P.n_eq = (int32_t)S.n_eq;
+        const int nd = grids[S.grid].ndim;
+        int64_t bs = 1, gs = 1;
+        int64_t stride[3];
+        for (int k = 2; k >= 0; --k) {
+            P.lo[k] = k < nd ? (int32_t)S.lo[k] : 0;
+            P.hi[k] = k < nd ? (int32_t)S.hi[k] : 1;
+            P.bstride[k] = (int32_t)bs;
+            stride[k] = gs;
+            bs *= P.hi[k] - P.lo[k];
+            gs *= G.shape[k];
+        }
+        for (int k = 0; k < 3; ++k) {
+            P.ilo[k] = P.lo[k];
+            P.ihi[k] = P.hi[k];
+        }
+        for (int t = 0; t < S.ntpl; ++t) {
+            P.doff[t] = P.boff[t] = 0;
+            for (int k = 0; k < 3; ++k) {
+                const int64_t o = k < nd ? S.off[t][k] : 0;
+                if (P.lo[k] + o < 0 || P.hi[k] - 1 + o >= G.shape[k] || o < -MF_R || o > MF_R) return false;
+                P.off[t][k] = (int32_t)o;
+                P.doff[t] += (int32_t)(o * stride[k]);
+                P.boff[t] += (int32_t)(o * P.bstride[k]);
+                P.ilo[k] = std::max<int32_t>(P.ilo[k], P.lo[k] + (int32_t)o);
+                P.ihi[k] = std::min<int32_t>(P.ihi[k], P.hi[k] + (int32_t)o);
+            }
+            P.val[t] = S.val[t];
+        }
+        // Aᵀu validity of template t for a column c: lo <= c - off_t < hi in every dim, i.e.
+        // off_t <= c - lo and off_t >= c - hi + 1.  With |off| <= MF_R both sides depend only on
+        // a = clamp(c - lo + MF_R + 1, 0, 2 MF_R + 1) and b = clamp(c - hi + MF_R + 1, ...):
+        // byte a of mlo / byte b of mhi hold the templates valid on that side.
+        for (int k = 0; k < 3; ++k) {
+            P.mlo[k] = P.mhi[k] = 0;
+            for (int a = 0; a <= 2 * MF_R + 1; ++a) {
+                uint64_t lo_bits = 0, hi_bits = 0;
+                for (int t = 0; t < S.ntpl; ++t) {
+                    if (P.off[t][k] <= a - MF_R - 1) lo_bits |= uint64_t(1) << t;
+                    if (P.off[t][k] >= a - MF_R) hi_bits |= uint64_t(1) << t;
+                }
+                P.mlo[k] |= lo_bits << (8 * a);
+                P.mhi[k] |= hi_bits << (8 * a);
+            }
+        }
+        G.part[G.nparts++] = d.n_parts++;
+    }
+    // node enumeration: the grids with parts, each starting on a MF_ALIGN boundary, so a block
+    // iteration (A·v) or a wave's 256 columns (Aᵀu) never spans two grids; they must cover every
+    // column (the Aᵀu kernel walks this enumeration)
+    int64_t node0 = 0, covered = 0;
+    for (int g = 0; g < n_grids; ++g) {
+        d.g[g].node0 = (int32_t)node0;
+        if (d.g[g].nparts) {
+            node0 += (d.g[g].nodes + MF_ALIGN - 1) / MF_ALIGN * MF_ALIGN;
+            covered += d.g[g].nodes;
+        }
+    }
+    d.nodes = node0;
+    return d.n_parts > 0 && covered == n_full && node0 < (int64_t(1) << 31);
+}
+
 }  // namespace
 
 void form_from_stencils(System& S, int64_t m, int64_t n_full, int32_t n_grids, const lsq_grid_desc* grids,
@@ -224,6 +332,7 @@ void form_from_stencils(System& S, int64_t m, int64_t n_full, int32_t n_grids, c
     if (herr) throw std::invalid_argument("lsq_set_matrix_stencil: " + std::to_string(herr) +
                                           " nonzero entries fall outside [0, n_full)");
     S.n_sorted_rows = npts;   // data rows: point order is random in space
+    S.mf = !S.dist && !S.comm && !S.virt && describe_stencil_operator(S.mfh, m, n_full, n_grids, grids, npts, n_stencil, st);
     finish_formation(S);
 }
 

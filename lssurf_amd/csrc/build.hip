@@ -198,7 +198,7 @@ __global__ __launch_bounds__(BLOCK) void k_slice_width(int64_t rows, int64_t nsl
         const int64_t r1 = r0 + SELL_C < rows ? r0 + SELL_C : rows;
         for (int64_t r = r0; r < r1; ++r) {
             const int64_t q = perm ? perm[r] : r;
-            w = max(w, rp[q + 1] - rp[q]);
+            if (q >= 0) w = max(w, rp[q + 1] - rp[q]);
         }
         wid[s] = w * SELL_C;
     }
@@ -211,12 +211,11 @@ __global__ __launch_bounds__(BLOCK) void k_sell_cols(int64_t rows, const int64_t
                                                      const int64_t* __restrict__ sp, int32_t* __restrict__ sci) {
     for (int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BLOCK) {
         const int64_t s = r / SELL_C, lane = r % SELL_C;
-        const int64_t q = perm ? perm[r] : r;
+        const int64_t q = perm ? perm[r] : r;   // q < 0: empty row
         const int64_t base = sp[s], W = (sp[s + 1] - base) / SELL_C;
-        const int64_t b = rp[q], L = rp[q + 1] - b;
+        const int64_t b = q >= 0 ? rp[q] : 0, L = q >= 0 ? rp[q + 1] - b : 0;
         for (int64_t k = 0; k < W; ++k) {
-            int32_t c = ci[b + (k < L ? k : L - 1)];
-            if (!L) c = 0;
+            int32_t c = L ? ci[b + (k < L ? k : L - 1)] : 0;
             sci[base + k * SELL_C + lane] = cmap && L ? cmap[c] : c;
         }
     }
@@ -240,6 +239,63 @@ __global__ __launch_bounds__(BLOCK) void k_row_keys(int64_t m, int64_t n_sorted,
     }
 }
 
+__global__ __launch_bounds__(BLOCK) void k_keep_list(int64_t n_full, const int32_t* __restrict__ colmap,
+                                                     int32_t* __restrict__ keep) {
+    for (int64_t f = (int64_t)blockIdx.x * BLOCK + threadIdx.x; f < n_full; f += (int64_t)gridDim.x * BLOCK) {
+        const int32_t c = colmap ? colmap[f] : (int32_t)f;
+        if (c >= 0) keep[c] = (int32_t)f;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_scatter_cs(int64_t n, const int32_t* __restrict__ keep,
+                                                      const double* __restrict__ cs, double* __restrict__ csf) {
+    for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLOCK)
+        csf[keep[j]] = cs[j];
+}
+
+// per stencil part: min and max of the row scale over its rows (block p -> part p)
+__global__ __launch_bounds__(BLOCK) void k_part_minmax(const MfDesc* __restrict__ d, const double* __restrict__ rs,
+                                                       double* __restrict__ out) {
+    __shared__ double lo[BLOCK], hi[BLOCK];
+    const MfPart& P = d->p[blockIdx.x];
+    double a = INFINITY, b = -INFINITY;
+    for (int64_t r = threadIdx.x; r < P.n_eq; r += BLOCK) {
+        const double x = rs[P.row0 + r];
+        a = fmin(a, x);
+        b = fmax(b, x);
+    }
+    lo[threadIdx.x] = a;
+    hi[threadIdx.x] = b;
+    __syncthreads();
+    for (int k = BLOCK / 2; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) {
+            lo[threadIdx.x] = fmin(lo[threadIdx.x], lo[threadIdx.x + k]);
+            hi[threadIdx.x] = fmax(hi[threadIdx.x], hi[threadIdx.x + k]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[2 * blockIdx.x] = lo[0];
+        out[2 * blockIdx.x + 1] = hi[0];
+    }
+}
+
+// position -> GdT row (compact column) of the node enumeration, -1 for padding / removed columns
+__global__ __launch_bounds__(BLOCK) void k_enum_perm(const MfDesc* __restrict__ d, int64_t ne,
+                                                     const int32_t* __restrict__ colmap, int32_t* __restrict__ perm) {
+    for (int64_t pos = (int64_t)blockIdx.x * BLOCK + threadIdx.x; pos < ne; pos += (int64_t)gridDim.x * BLOCK) {
+        int32_t q = -1;
+        for (int g = 0; g < d->n_grids; ++g) {
+            const MfGrid& G = d->g[g];
+            if (G.nparts && pos >= G.node0 && pos < (int64_t)G.node0 + G.nodes) {
+                const int64_t f = G.col0 + (pos - G.node0);
+                q = colmap ? colmap[f] : (int32_t)f;
+            }
+        }
+        perm[pos] = q;
+    }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_invert(int64_t m, const int32_t* __restrict__ perm,
                                                   int32_t* __restrict__ inv) {
     for (int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x; r < m; r += (int64_t)gridDim.x * BLOCK)
@@ -255,15 +311,19 @@ __global__ __launch_bounds__(BLOCK) void k_sell_vals(int64_t rows, const int64_t
                                                      const int64_t* __restrict__ sp, double* __restrict__ sval) {
     for (int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BLOCK) {
         const int64_t s = r / SELL_C, lane = r % SELL_C;
-        const int64_t q = perm ? perm[r] : r;   // CSR row
+        const int64_t q = perm ? perm[r] : r;   // CSR row (< 0: empty row)
         const int64_t base = sp[s], W = (sp[s + 1] - base) / SELL_C;
-        const int64_t b = rp[q], L = rp[q + 1] - b;
+        const int64_t b = q >= 0 ? rp[q] : 0, L = q >= 0 ? rp[q + 1] - b : 0;
         for (int64_t k = 0; k < W; ++k) {
             double x = 0.0;
             if (k < L) {
                 const int32_t c = ci[b + k];
                 // A: row scale of q, col scale of c.  AT: row scale of c, col scale of q.
-                x = transposed ? (g[b + k] * rowsc[c]) * colsc[q] : (g[b + k] * rowsc[q]) * colsc[c];
+                // colsc == nullptr: no column factor (the stencil operator applies cs itself)
+                if (transposed)
+                    x = colsc ? (g[b + k] * rowsc[c]) * colsc[q] : g[b + k] * rowsc[c];
+                else
+                    x = colsc ? (g[b + k] * rowsc[q]) * colsc[c] : g[b + k] * rowsc[q];
             }
             sval[base + k * SELL_C + lane] = x;
         }
@@ -357,13 +417,15 @@ void check_err(BuildErr* d_err, hipStream_t s, const char* stage) {
     }
 }
 
-void build_sell(Sell& S, const Csr& C, const int32_t* cmap, hipStream_t st) {
-    S.rows = C.m;
-    S.nslices = (C.m + SELL_C - 1) / SELL_C;
+// SELL copy of `rows` rows: SELL row r = CSR row perm[r] of C (S.perm; identity if empty; < 0
+// = empty row); column ids optionally mapped through cmap.
+void build_sell(Sell& S, const Csr& C, int64_t rows, const int32_t* cmap, hipStream_t st) {
+    S.rows = rows;
+    S.nslices = (rows + SELL_C - 1) / SELL_C;
     S.sp.alloc(S.nslices + 1);
     S.sp.zero(st);
     const int32_t* perm = S.perm.n ? S.perm.p : nullptr;
-    hipLaunchKernelGGL(k_slice_width, dim3(grid_for(S.nslices)), dim3(BLOCK), 0, st, C.m, S.nslices, C.rp.p, perm,
+    hipLaunchKernelGGL(k_slice_width, dim3(grid_for(S.nslices)), dim3(BLOCK), 0, st, rows, S.nslices, C.rp.p, perm,
                        S.sp.p);
     KERNEL_CHECK();
     S.nent = exclusive_scan_i64(S.sp.p, S.nslices + 1, st);
@@ -373,14 +435,14 @@ void build_sell(Sell& S, const Csr& C, const int32_t* cmap, hipStream_t st) {
     // give them column 0 and value 0 so any read of them is in bounds and contributes nothing
     S.ci.zero(st);
     S.val.zero(st);
-    hipLaunchKernelGGL(k_sell_cols, dim3(grid_for(C.m)), dim3(BLOCK), 0, st, C.m, C.rp.p, C.ci.p, perm, cmap, S.sp.p,
+    hipLaunchKernelGGL(k_sell_cols, dim3(grid_for(rows)), dim3(BLOCK), 0, st, rows, C.rp.p, C.ci.p, perm, cmap, S.sp.p,
                        S.ci.p);
     KERNEL_CHECK();
 }
 
 // A's SELL row order (k_row_keys): one radix sort of 64-bit keys.
-void locality_order(const Csr& G, int64_t n_sorted, DBuf<int32_t>& perm, DBuf<int32_t>& inv, hipStream_t st) {
-    const int64_t m = G.m;
+void locality_order(const Csr& G, int64_t m, int64_t n_sorted, DBuf<int32_t>& perm, DBuf<int32_t>& inv,
+                    hipStream_t st) {
     perm.alloc(std::max<int64_t>(m, 1));
     inv.alloc(std::max<int64_t>(m, 1));
     if (m == 0) return;
@@ -453,43 +515,101 @@ void form_from_coo(System& S, int64_t m, int64_t n_full, int64_t nnz, const int6
     tv.release();
     off.release();
     S.n_sorted_rows = 0;
+    S.mf = false;   // generic operator: assembled SELL only
     finish_formation(S);
 }
 
 // G (canonical CSR, set) -> GT, SELL copies, default scaling state.
-void finish_formation(System& S) {
-    hipStream_t st = S.stream;
-    Csr& G = S.G;
-    const int64_t m = G.m, n = G.n;
+namespace {
+
+// CSR transpose of the first `rows` rows of G (entries of a column in ascending row order).
+void transpose_rows(const Csr& G, int64_t rows, Csr& T, hipStream_t st) {
+    const int64_t n = G.n;
     DBuf<BuildErr> err(1);
     err.zero(st);
-    // transpose
-    Csr& T = S.GT;
     T.m = n;
-    T.n = m;
-    T.nnz = G.nnz;
+    T.n = rows;
     DBuf<unsigned long long> ccnt(n + 1), ccur(n + 1);
     ccnt.zero(st);
     ccur.zero(st);
-    hipLaunchKernelGGL(k_col_count, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, G.rp.p, G.ci.p, ccnt.p);
+    hipLaunchKernelGGL(k_col_count, dim3(grid_for(rows)), dim3(BLOCK), 0, st, rows, G.rp.p, G.ci.p, ccnt.p);
     KERNEL_CHECK();
     T.rp.alloc(n + 1);
     hipLaunchKernelGGL(k_u64_to_i64, dim3(grid_for(n + 1)), dim3(BLOCK), 0, st, n + 1, ccnt.p, T.rp.p);
     KERNEL_CHECK();
-    exclusive_scan_i64(T.rp.p, n + 1, st);
+    T.nnz = exclusive_scan_i64(T.rp.p, n + 1, st);
     T.ci.alloc(std::max<int64_t>(T.nnz, 1));
     T.val.alloc(std::max<int64_t>(T.nnz, 1));
-    hipLaunchKernelGGL(k_t_scatter, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, G.rp.p, G.ci.p, G.val.p, T.rp.p, ccur.p,
-                       T.ci.p, T.val.p);
+    hipLaunchKernelGGL(k_t_scatter, dim3(grid_for(rows)), dim3(BLOCK), 0, st, rows, G.rp.p, G.ci.p, G.val.p, T.rp.p,
+                       ccur.p, T.ci.p, T.val.p);
     KERNEL_CHECK();
     hipLaunchKernelGGL(k_seg_sort, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, T.rp.p, T.ci.p, T.val.p, err.p);
     KERNEL_CHECK();
-    check_err(err.p, st, "lsq_set_matrix_coo (transpose)");
+    check_err(err.p, st, "matrix transpose");
+}
 
+}  // namespace
+
+// Assembled SELL copies of the whole operator (A rows grouped by length, data rows by first
+// column; AT's column ids = A's SELL row ids).
+void ensure_sell(System& S) {
+    if (S.sell_built) return;
+    hipStream_t st = S.stream;
     DBuf<int32_t> inv;
-    locality_order(G, S.n_sorted_rows, S.A.perm, inv, st);
-    build_sell(S.A, G, nullptr, st);
-    build_sell(S.AT, T, inv.p, st);   // AT's column ids = A's SELL row ids
+    locality_order(S.G, S.G.m, S.n_sorted_rows, S.A.perm, inv, st);
+    build_sell(S.A, S.G, S.G.m, nullptr, st);
+    build_sell(S.AT, S.GT, S.GT.m, inv.p, st);
+    HIP_CHECK(hipStreamSynchronize(st));
+    S.sell_built = true;
+    S.cs_mode = -1;   // values are filled by the next refresh
+    S.iter_ready = false;
+}
+
+namespace {
+
+// Data rows of a structured system: Ad (SELL rows = data rows by first column, full column ids)
+// and ATd (SELL rows = node-enumeration positions, column ids = Ad row positions).
+void build_stencil_operator(System& S) {
+    hipStream_t st = S.stream;
+    const int64_t npts = S.mfh.npts, nf = S.n_full, n = S.G.n;
+    S.keep.alloc(std::max<int64_t>(n, 1));
+    hipLaunchKernelGGL(k_keep_list, dim3(grid_for(nf)), dim3(BLOCK), 0, st, nf, S.have_colmap ? S.colmap.p : nullptr,
+                       S.keep.p);
+    KERNEL_CHECK();
+    DBuf<int32_t> inv;
+    locality_order(S.G, npts, npts, S.Ad.perm, inv, st);
+    build_sell(S.Ad, S.G, npts, S.keep.p, st);
+    transpose_rows(S.G, npts, S.GdT, st);
+    // ATd row = node-enumeration position (MfDesc): GdT row of its column, -1 for alignment
+    // padding and removed columns
+    S.mfd.alloc(1);
+    S.mfd.upload(&S.mfh, 1, st);
+    const int64_t ne = S.mfh.nodes;
+    S.ATd.perm.alloc(std::max<int64_t>(ne, 1));
+    hipLaunchKernelGGL(k_enum_perm, dim3(grid_for(ne)), dim3(BLOCK), 0, st, S.mfd.p, ne,
+                       S.have_colmap ? S.colmap.p : nullptr, S.ATd.perm.p);
+    KERNEL_CHECK();
+    build_sell(S.ATd, S.GdT, ne, inv.p, st);
+    S.csf.alloc(std::max<int64_t>(nf, 1));
+    S.zv.alloc(std::max<int64_t>(nf, 1));
+    S.zv.zero(st);
+    HIP_CHECK(hipStreamSynchronize(st));
+}
+
+}  // namespace
+
+void finish_formation(System& S) {
+    hipStream_t st = S.stream;
+    Csr& G = S.G;
+    const int64_t m = G.m, n = G.n;
+    transpose_rows(G, m, S.GT, st);
+    S.sell_built = false;
+    S.A = Sell();
+    S.AT = Sell();
+    if (S.mf)
+        build_stencil_operator(S);
+    else
+        ensure_sell(S);
 
     // default scaling state: weights 1, all rows kept, no preconditioner
     S.roww.alloc(m);
@@ -530,12 +650,39 @@ void scaling_finish_cs(System& S) {
 void scaling_fill_values(System& S, int precond) {
     hipStream_t st = S.stream;
     const int64_t m = S.G.m, n = S.G.n;
-    hipLaunchKernelGGL(k_sell_vals, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, S.G.rp.p, S.G.ci.p, S.G.val.p, S.rs.p,
-                       S.cs.p, 0, S.A.perm.p, S.A.sp.p, S.A.val.p);
-    KERNEL_CHECK();
-    hipLaunchKernelGGL(k_sell_vals, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, S.GT.rp.p, S.GT.ci.p, S.GT.val.p, S.rs.p,
-                       S.cs.p, 1, nullptr, S.AT.sp.p, S.AT.val.p);
-    KERNEL_CHECK();
+    if (S.sell_built) {
+        hipLaunchKernelGGL(k_sell_vals, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, S.G.rp.p, S.G.ci.p, S.G.val.p,
+                           S.rs.p, S.cs.p, 0, S.A.perm.p, S.A.sp.p, S.A.val.p);
+        KERNEL_CHECK();
+        hipLaunchKernelGGL(k_sell_vals, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, S.GT.rp.p, S.GT.ci.p, S.GT.val.p,
+                           S.rs.p, S.cs.p, 1, nullptr, S.AT.sp.p, S.AT.val.p);
+        KERNEL_CHECK();
+    }
+    if (S.mf) {   // data rows carry the row scale only; the stencil kernels apply cs themselves
+        const int64_t npts = S.mfh.npts, nf = S.n_full;
+        hipLaunchKernelGGL(k_sell_vals, dim3(grid_for(npts)), dim3(BLOCK), 0, st, npts, S.G.rp.p, S.G.ci.p,
+                           S.G.val.p, S.rs.p, nullptr, 0, S.Ad.perm.p, S.Ad.sp.p, S.Ad.val.p);
+        KERNEL_CHECK();
+        hipLaunchKernelGGL(k_sell_vals, dim3(grid_for(S.ATd.rows)), dim3(BLOCK), 0, st, S.ATd.rows, S.GdT.rp.p,
+                           S.GdT.ci.p, S.GdT.val.p, S.rs.p, nullptr, 1, S.ATd.perm.p, S.ATd.sp.p, S.ATd.val.p);
+        KERNEL_CHECK();
+        S.csf.zero(st);
+        hipLaunchKernelGGL(k_scatter_cs, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, S.keep.p, S.cs.p, S.csf.p);
+        KERNEL_CHECK();
+        // parts whose rows share one row scale skip the per-row scale loads in the iteration
+        const int np = S.mfh.n_parts;
+        DBuf<double> mm(2 * np);
+        hipLaunchKernelGGL(k_part_minmax, dim3(np), dim3(BLOCK), 0, st, S.mfd.p, S.rs.p, mm.p);
+        KERNEL_CHECK();
+        std::vector<double> h(2 * np);
+        mm.download(h.data(), 2 * np, st);
+        HIP_CHECK(hipStreamSynchronize(st));
+        for (int p = 0; p < np; ++p) {
+            S.mfh.p[p].wconst = h[2 * p] == h[2 * p + 1] ? 1 : 0;
+            S.mfh.p[p].w = h[2 * p];
+        }
+        S.mfd.upload(&S.mfh, 1, st);
+    }
     S.rs_dirty = false;
     S.cs_mode = precond;
     S.iter_ready = false;
@@ -579,8 +726,10 @@ void relabel_columns(System& S, const int32_t* h_map, int64_t n_local) {
     if (h) throw std::invalid_argument("lsq_dist_set_layout: a referenced column has no local index");
     S.G.n = n_local;
     S.GT = Csr{};
-    S.A = Sell{};
-    S.AT = Sell{};
+    S.mf = false;   // distributed ranks stream the assembled local operator
+    S.Ad = Sell{};
+    S.ATd = Sell{};
+    S.GdT = Csr{};
     finish_formation(S);
 }
 

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(BLOCK) void k_init_u(int64_t m, int64_t nslices, co
                                                   const double* __restrict__ y0, const int32_t* __restrict__ perm,
                                                   double* __restrict__ u, double* __restrict__ bw, double* part_u,
                                                   double* part_b) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
     double su = 0.0, sb = 0.0;
     for (int64_t s = (int64_t)blockIdx.x * 4 + wid; s < nslices; s += (int64_t)gridDim.x * 4) {
         const int64_t row = s * SELL_C + lane;
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(BLOCK) void k_xw_spmv(const LsqState* __restrict__ 
     const int bid = blockIdx.x - gX, gA = gridDim.x - gX;
     const double alpha = st->alpha, ib = st->inv_beta;
     const double ia = xs_scaled ? st->inv_alpha : 1.0;   // precond 2 gathers z = R⁻¹ ṽ/α
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
     double su = 0.0;
     for (int64_t s = (int64_t)bid * 4 + wid; s < nslices; s += (int64_t)gA * 4) {
         const int64_t row = s * SELL_C + lane;
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmtv(const LsqState* __restrict__ st
                                                  const double* __restrict__ vin, double* __restrict__ vout,
                                                  double* part_v, int raw) {
     if (st->stop) return;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
     const double ib = st->inv_beta, beta = st->beta, ia = st->inv_alpha;
     const bool skip = st->skip_v;
     double sv = 0.0;
@@ -358,12 +358,22 @@ __global__ __launch_bounds__(BLOCK) void k_scatter_add(int64_t cnt, const int32_
         dst[idx[k]] += src[k];
 }
 
+#include "lsqr_mf.inc"
+
 struct Grids {
     int gA, gT, gX, gR, gRT, gE;
+    int gD, gS, gM, gXf;   // stencil operator: data-row blocks, node blocks, Aᵀu blocks, x/w blocks
 };
 
 Grids grids_for(const System& S) {
     Grids g;
+    g.gD = g.gS = g.gM = g.gXf = 1;
+    if (S.mf) {
+        g.gD = (int)std::min<int64_t>(std::max<int64_t>((S.Ad.nslices + 3) / 4, 1), NPART / 4);
+        g.gS = (int)std::min<int64_t>(std::max<int64_t>(S.mfh.nodes / MF_ALIGN, 1), NPART - g.gD);
+        g.gM = (int)std::min<int64_t>(std::max<int64_t>(S.mfh.nodes / (SELL_C * MF_NPT) / 4, 1), NPART);
+        g.gXf = grid_for(S.n_full, BLOCK * 4, NPART);
+    }
     g.gA = (int)std::min<int64_t>(std::max<int64_t>((S.A.nslices + 3) / 4, 1), NPART);
     g.gT = (int)std::min<int64_t>(std::max<int64_t>((S.AT.nslices + 3) / 4, 1), NPART);
     g.gX = grid_for(S.ncols_own(), BLOCK * 4, NPART);
@@ -374,7 +384,7 @@ Grids grids_for(const System& S) {
 }
 
 void ensure_workspace(System& S) {
-    const int64_t m = S.G.m, n = std::max<int64_t>(S.G.n, 1);
+    const int64_t m = S.G.m, n = std::max<int64_t>(S.vlen(), 1);
     if (S.u.n != std::max<int64_t>(m, 1)) {
         S.u.alloc(std::max<int64_t>(m, 1));
         S.bw.alloc(std::max<int64_t>(m, 1));
@@ -422,8 +432,32 @@ void launch_iteration(System& S, const Grids& g, int p, int precond) {
     }
 }
 
+// one iteration on the structured stencil operator (full column space, zv = cs∘ṽ)
+void launch_iteration_mf(System& S, const Grids& g, int p) {
+    hipStream_t st = S.stream;
+    double* vt = p ? S.vb1.p : S.vb0.p;
+    double* vo = p ? S.vb0.p : S.vb1.p;
+    hipLaunchKernelGGL(k_mf_fwd, dim3(g.gXf + g.gD + g.gS), dim3(BLOCK), 0, st, S.st.p, g.gXf, g.gD, S.n_full, S.y.p,
+                       S.w.p, vt, S.mfh.npts, S.Ad.nslices, S.Ad.sp.p, S.Ad.ci.p, S.Ad.val.p, S.mfd.p, S.zv.p, S.rs.p,
+                       S.u.p, S.part_u.p, S.part_w.p);
+    hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gD + g.gS, S.part_b.p, 0, 0,
+                       nullptr);
+    hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.sp.p, S.ATd.ci.p, S.ATd.val.p,
+                       S.mfd.p, S.u.p, S.rs.p, S.csf.p, vt, vo, S.zv.p, S.part_v.p);
+    hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gM, S.part_w.p, g.gXf, 0, nullptr);
+}
+
 // final x/w update of a solve that stopped on the last iteration of a batch (newest ṽ in vb0)
-void launch_flush(System& S, const Grids& g) {
+void launch_flush(System& S, const Grids& g, bool mf) {
+    if (mf) {
+        hipLaunchKernelGGL(k_mf_fwd, dim3(g.gXf + g.gD + g.gS), dim3(BLOCK), 0, S.stream, S.st.p, g.gXf, g.gD,
+                           S.n_full, S.y.p, S.w.p, S.vb0.p, S.mfh.npts, S.Ad.nslices, S.Ad.sp.p, S.Ad.ci.p, S.Ad.val.p,
+                           S.mfd.p, S.zv.p, S.rs.p, S.u.p, S.part_u.p, S.part_w.p);
+        hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, S.stream, S.st.p, S.part_u.p, g.gD + g.gS, S.part_b.p, 0, 0,
+                           nullptr);
+        KERNEL_CHECK();
+        return;
+    }
     hipLaunchKernelGGL(k_xw_spmv, dim3(g.gX + g.gA), dim3(BLOCK), 0, S.stream, S.st.p, g.gX, S.ncols_own(), S.y.p, S.w.p,
                        S.vb0.p, S.vb0.p, 1, S.G.m, S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p, S.u.p, S.part_u.p,
                        S.part_w.p);
@@ -436,7 +470,56 @@ void launch_flush(System& S, const Grids& g) {
 // Initialise the LSQR state from rhs b (host, length m, unweighted) and optional warm start
 // x0 (host, length n, or nullptr).  Mirrors scipy lsqr's set-up block for the operator A·M
 // (M = diag(cs) for precond 0/1, M = R⁻¹ for precond 2).
-void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts& o, bool no_stop) {
+namespace {
+
+// lsqr_init on the structured stencil operator (full column space)
+void lsqr_init_mf(System& S, const double* h_b, const double* h_x0, const lsq_opts& o, bool no_stop) {
+    hipStream_t st = S.stream;
+    ensure_workspace(S);
+    const Grids g = grids_for(S);
+    const int64_t m = S.G.m, n = S.G.n, nf = S.n_full;
+    DBuf<double> db(std::max<int64_t>(m, 1));
+    db.upload(h_b, m, st);
+    DBuf<double> dx0, dy0, dz0;
+    if (h_x0) {
+        dx0.alloc(std::max<int64_t>(n, 1));
+        dx0.upload(h_x0, n, st);
+        dy0.alloc(std::max<int64_t>(nf, 1));
+        dz0.alloc(std::max<int64_t>(nf, 1));
+        dy0.zero(st);
+        dz0.zero(st);
+        hipLaunchKernelGGL(k_mf_warm, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, S.keep.p, dx0.p, S.cs.p, dy0.p, dz0.p);
+        KERNEL_CHECK();
+    }
+    LsqState h{};
+    h.atol = o.atol;
+    h.btol = o.btol;
+    h.ctol = o.conlim > 0 ? 1.0 / o.conlim : 0.0;
+    h.maxit = o.maxit > 0 ? o.maxit : 4 * std::max<int64_t>(n, 1);
+    h.no_stop = no_stop ? 1 : 0;
+    h.cs2 = -1.0;
+    HIP_CHECK(hipMemcpyAsync(S.st.p, &h, sizeof(h), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_mf_init_u, dim3(g.gD + g.gS), dim3(BLOCK), 0, st, g.gD, S.mfh.npts, S.Ad.nslices, S.Ad.sp.p,
+                       S.Ad.ci.p, S.Ad.val.p, S.Ad.perm.p, S.mfd.p, h_x0 ? dz0.p : nullptr, S.rs.p, db.p, S.u.p, S.bw.p,
+                       S.part_u.p, S.part_b.p);
+    KERNEL_CHECK();
+    hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gD + g.gS, S.part_b.p,
+                       g.gD + g.gS, 1, nullptr);
+    S.vb1.zero(st);
+    hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.sp.p, S.ATd.ci.p, S.ATd.val.p,
+                       S.mfd.p, S.u.p, S.rs.p, S.csf.p, S.vb1.p, S.vb0.p, S.zv.p, S.part_v.p);
+    hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gM, S.part_w.p, g.gXf, 1, nullptr);
+    hipLaunchKernelGGL(k_init_w, dim3(g.gXf), dim3(BLOCK), 0, st, S.st.p, nf, S.vb0.p, h_x0 ? dy0.p : nullptr, S.w.p,
+                       S.y.p, S.part_w.p);
+    KERNEL_CHECK();
+    HIP_CHECK(hipStreamSynchronize(st));
+    S.iter_parity = 0;
+}
+
+}  // namespace
+
+void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts& o, bool no_stop, bool mf) {
+    if (mf) return lsqr_init_mf(S, h_b, h_x0, o, no_stop);
     hipStream_t st = S.stream;
     ensure_workspace(S);
     const Grids g = grids_for(S);
@@ -500,45 +583,76 @@ struct GraphCache {
     const System* sys = nullptr;
     const void* key = nullptr;   // S.u.p identifies the workspace generation
     int batch = 0;
-    int precond = -1;
+    int mode = -1;               // precond * 2 + stencil-operator flag
     hipGraphExec_t exec = nullptr;
 };
 thread_local GraphCache g_cache;
 
+void launch_any(System& S, const Grids& g, int p, int precond, bool mf) {
+    if (mf)
+        launch_iteration_mf(S, g, p);
+    else
+        launch_iteration(S, g, p, precond);
+}
+
 // run `count` iterations starting at parity S.iter_parity (count even when graphs are used)
-void run_batch(System& S, int count, bool use_graph, int precond) {
+void run_batch(System& S, int count, bool use_graph, int precond, bool mf) {
     const Grids g = grids_for(S);
+    const int mode = precond * 2 + (mf ? 1 : 0);
     if (use_graph && count % 2 == 0 && S.iter_parity == 0) {
         GraphCache& c = g_cache;
-        if (c.exec == nullptr || c.sys != &S || c.key != (const void*)S.u.p || c.batch != count ||
-            c.precond != precond) {
+        if (c.exec == nullptr || c.sys != &S || c.key != (const void*)S.u.p || c.batch != count || c.mode != mode) {
             if (c.exec) (void)hipGraphExecDestroy(c.exec);
             c.exec = nullptr;
             hipGraph_t graph;
             HIP_CHECK(hipStreamBeginCapture(S.stream, hipStreamCaptureModeThreadLocal));
-            for (int i = 0; i < count; ++i) launch_iteration(S, g, i & 1, precond);
+            for (int i = 0; i < count; ++i) launch_any(S, g, i & 1, precond, mf);
             HIP_CHECK(hipStreamEndCapture(S.stream, &graph));
             HIP_CHECK(hipGraphInstantiate(&c.exec, graph, nullptr, nullptr, 0));
             HIP_CHECK(hipGraphDestroy(graph));
             c.sys = &S;
             c.key = S.u.p;
             c.batch = count;
-            c.precond = precond;
+            c.mode = mode;
         }
         HIP_CHECK(hipGraphLaunch(c.exec, S.stream));
         return;
     }
     for (int i = 0; i < count; ++i) {
-        launch_iteration(S, g, S.iter_parity, precond);
+        launch_any(S, g, S.iter_parity, precond, mf);
         S.iter_parity ^= 1;
     }
     KERNEL_CHECK();
 }
 
-double bytes_per_iter(const System& S) {
+// Algorithmic HBM bytes per launch of the two streaming kernels (DESIGN.md §Byte model).
+// Assembled SELL: x/w+A·v = 12Z + 16m + 48n, Aᵀu = 12Z + 8m + 16n (Z = nnz, 12 B per entry).
+// Stencil operator: x/w+A·v = 48 n_f + 12 Z_d + 16 m_d + 24 m_s, Aᵀu = 32 n_f + 12 Z_d + 8 m_d + 16 m_s
+// (Z_d entries of the m_d data rows; m_s stencil rows: rs + u r/w, rs + u; per column y, w r/w,
+// ṽ, zv gathered once / cs, ṽ in, ṽ out, zv out).
+void kernel_bytes(const System& S, bool mf, double out[2]) {
+    if (mf) {
+        const double nf = (double)S.n_full, md = (double)S.mfh.npts, ms = (double)(S.G.m - S.mfh.npts);
+        double zd = 0.0;
+        zd = (double)S.GdT.nnz;
+        out[0] = 48.0 * nf + 12.0 * zd + 16.0 * md + 24.0 * ms;
+        out[1] = 32.0 * nf + 12.0 * zd + 8.0 * md + 16.0 * ms;
+        return;
+    }
     const double Z = (double)S.G.nnz, m = (double)S.G.m, n = (double)S.G.n;
-    return 24.0 * Z + 24.0 * m + 64.0 * n;   // DESIGN.md §Byte model
+    out[0] = 12.0 * Z + 16.0 * m + 48.0 * n;
+    out[1] = 12.0 * Z + 8.0 * m + 16.0 * n;
 }
+
+}  // namespace
+
+double bytes_per_iter(const System& S, bool mf) {
+    double b[2];
+    kernel_bytes(S, mf, b);
+    return b[0] + b[1];
+}
+
+namespace {
 
 void fill_stats(const LsqState& h, lsq_stats* s) {
     s->iters = h.itn;
@@ -551,7 +665,10 @@ void fill_stats(const LsqState& h, lsq_stats* s) {
     s->xnorm = h.xnorm;
 }
 
-void prepare(System& S, int precond) {
+bool use_mf(const System& S, const lsq_opts& o) { return S.mf && o.op == 0 && o.precond != 2 && !S.dist; }
+
+void prepare(System& S, int precond, bool mf) {
+    if (!mf) ensure_sell(S);
     refresh_scaling(S, precond);
     if (precond == 2 && !S.dense_valid) dense_factor(S);
 }
@@ -566,8 +683,9 @@ void graph_cache_drop(const System* S) {
 }
 
 int lsqr_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq_stats* stats) {
-    prepare(S, o.precond);
-    lsqr_init(S, h_b, o.use_x0 ? h_x : nullptr, o, false);
+    const bool mf = use_mf(S, o);
+    prepare(S, o.precond, mf);
+    lsqr_init(S, h_b, o.use_x0 ? h_x : nullptr, o, false, mf);
     int batch = o.batch > 0 ? o.batch : 16;
     batch += batch & 1;
     hipEvent_t e0, e1;
@@ -578,18 +696,20 @@ int lsqr_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq
     HIP_CHECK(hipMemcpyAsync(&h, S.st.p, sizeof(h), hipMemcpyDeviceToHost, S.stream));
     HIP_CHECK(hipStreamSynchronize(S.stream));
     while (!h.stop) {
-        run_batch(S, batch, o.use_graph != 0, o.precond);
+        run_batch(S, batch, o.use_graph != 0, o.precond, mf);
         HIP_CHECK(hipMemcpyAsync(&h, S.st.p, sizeof(h), hipMemcpyDeviceToHost, S.stream));
         HIP_CHECK(hipStreamSynchronize(S.stream));
     }
     const Grids g = grids_for(S);
     if (!h.finished) {   // stop on the last iteration of a batch: apply its x/w update
         S.iter_parity = 0;
-        launch_flush(S, g);
+        launch_flush(S, g, mf);
     }
     HIP_CHECK(hipEventRecord(e1, S.stream));
     const int64_t n = S.G.n;
-    if (o.precond == 2)
+    if (mf)
+        hipLaunchKernelGGL(k_mf_x, dim3(grid_for(n)), dim3(BLOCK), 0, S.stream, n, S.keep.p, S.y.p, S.csf.p, S.vb1.p);
+    else if (o.precond == 2)
         hipLaunchKernelGGL(k_gemv_upper, dim3(g.gR), dim3(BLOCK), 0, S.stream, S.dRi.p, n, S.dense_ld, S.y.p, nullptr,
                            2, S.vb1.p);
     else
@@ -605,19 +725,22 @@ int lsqr_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq
     if (stats) {
         fill_stats(h, stats);
         stats->time_s = ms * 1e-3;
-        stats->bytes_per_iter = bytes_per_iter(S);
+        stats->bytes_per_iter = bytes_per_iter(S, mf);
     }
     S.iter_ready = false;   // the solve consumed the iteration state
     return h.istop == 7 ? 1 : 0;
 }
 
 int lsqr_iterate(System& S, const double* h_b, int64_t iters, const lsq_opts& o, lsq_stats* stats) {
-    prepare(S, o.precond);
-    if (!S.iter_ready) {
+    const bool mf = use_mf(S, o);
+    const int mode = o.precond * 2 + (mf ? 1 : 0);
+    prepare(S, o.precond, mf);
+    if (!S.iter_ready || S.iter_mode != mode) {
         lsq_opts oo = o;
         oo.maxit = INT64_MAX / 4;
-        lsqr_init(S, h_b, nullptr, oo, true);
+        lsqr_init(S, h_b, nullptr, oo, true, mf);
         S.iter_ready = true;
+        S.iter_mode = mode;
     }
     int batch = o.batch > 0 ? o.batch : 16;
     batch += batch & 1;
@@ -628,7 +751,7 @@ int lsqr_iterate(System& S, const double* h_b, int64_t iters, const lsq_opts& o,
     int64_t left = iters;
     while (left > 0) {
         const int c = (int)std::min<int64_t>(left, batch);
-        run_batch(S, c, o.use_graph != 0 && c == batch, o.precond);
+        run_batch(S, c, o.use_graph != 0 && c == batch, o.precond, mf);
         left -= c;
     }
     HIP_CHECK(hipEventRecord(e1, S.stream));
@@ -642,14 +765,20 @@ int lsqr_iterate(System& S, const double* h_b, int64_t iters, const lsq_opts& o,
     if (stats) {
         fill_stats(h, stats);
         stats->time_s = ms * 1e-3;
-        stats->bytes_per_iter = bytes_per_iter(S);
+        stats->bytes_per_iter = bytes_per_iter(S, mf);
     }
     return 0;
 }
 
-// Time each iteration kernel in isolation (reps launches, HIP events on the handle's stream).
-// Destroys the iteration state; used by bench.py for the per-kernel roofline.
-void lsqr_profile(System& S, int reps, double* ms_out /* [4]: xw_spmv, spmtv, beta, givens */) {
+// Time each iteration kernel of operator `op` in isolation (reps launches, HIP events on the
+// handle's stream) + algorithmic bytes per launch.  Destroys the iteration state; used by
+// bench.py for the per-kernel roofline.
+void lsqr_profile(System& S, int reps, int op, double* out /* [8] */) {
+    lsq_opts o;
+    lsq_default_opts(&o);
+    o.op = op;
+    const bool mf = use_mf(S, o);
+    if (!S.dist) prepare(S, 1, mf);   // a distributed rank keeps the scaling its group filled
     ensure_workspace(S);
     const Grids g = grids_for(S);
     hipEvent_t e0, e1;
@@ -659,33 +788,50 @@ void lsqr_profile(System& S, int reps, double* ms_out /* [4]: xw_spmv, spmtv, be
     h.alpha = 1.0; h.inv_alpha = 1.0; h.beta = 1.0; h.inv_beta = 1.0; h.have_xw = 1; h.t1 = 1e-3; h.t2 = -1e-3;
     h.maxit = INT64_MAX / 4; h.no_stop = 1; h.bnorm = 1.0; h.cs2 = -1.0;
     HIP_CHECK(hipMemcpyAsync(S.st.p, &h, sizeof(h), hipMemcpyHostToDevice, S.stream));
+    S.vb0.zero(S.stream);
+    S.vb1.zero(S.stream);
+    S.u.zero(S.stream);
+    S.w.zero(S.stream);
+    S.y.zero(S.stream);
+    if (mf) S.zv.zero(S.stream);
+    const int nu = mf ? g.gD + g.gS : g.gA, nv = mf ? g.gM : g.gT, nx = mf ? g.gXf : g.gX;
     for (int k = 0; k < 4; ++k) {
         for (int pass = 0; pass < 2; ++pass) {   // pass 0 = warm-up
             HIP_CHECK(hipEventRecord(e0, S.stream));
             for (int r = 0; r < reps; ++r) {
-                if (k == 0)
+                if (k == 0 && mf)
+                    hipLaunchKernelGGL(k_mf_fwd, dim3(g.gXf + g.gD + g.gS), dim3(BLOCK), 0, S.stream, S.st.p, g.gXf,
+                                       g.gD, S.n_full, S.y.p, S.w.p, S.vb0.p, S.mfh.npts, S.Ad.nslices, S.Ad.sp.p,
+                                       S.Ad.ci.p, S.Ad.val.p, S.mfd.p, S.zv.p, S.rs.p, S.u.p, S.part_u.p, S.part_w.p);
+                else if (k == 0)
                     hipLaunchKernelGGL(k_xw_spmv, dim3(g.gX + g.gA), dim3(BLOCK), 0, S.stream, S.st.p, g.gX, S.G.n,
                                        S.y.p, S.w.p, S.vb0.p, S.vb0.p, 1, S.G.m, S.A.nslices, S.A.sp.p, S.A.ci.p,
                                        S.A.val.p, S.u.p, S.part_u.p, S.part_w.p);
+                else if (k == 1 && mf)
+                    hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, S.stream, S.st.p, S.ATd.sp.p,
+                                       S.ATd.ci.p, S.ATd.val.p, S.mfd.p, S.u.p, S.rs.p, S.csf.p, S.vb0.p, S.vb1.p,
+                                       S.zv.p, S.part_v.p);
                 else if (k == 1)
                     hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, S.stream, S.st.p, S.G.n, S.AT.nslices,
                                        S.AT.sp.p, S.AT.ci.p, S.AT.val.p, S.u.p, S.vb0.p, S.vb1.p, S.part_v.p, 0);
                 else if (k == 2)
-                    hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, S.stream, S.st.p, S.part_u.p, g.gA,
+                    hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, S.stream, S.st.p, S.part_u.p, nu,
                                        S.part_b.p, 0, 2, nullptr);
                 else
-                    hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, S.stream, S.st.p, S.part_v.p, g.gT,
-                                       S.part_w.p, g.gX, 2, nullptr);
+                    hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, S.stream, S.st.p, S.part_v.p, nv,
+                                       S.part_w.p, nx, 2, nullptr);
             }
             HIP_CHECK(hipEventRecord(e1, S.stream));
             HIP_CHECK(hipEventSynchronize(e1));
         }
         float ms = 0.f;
         HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-        ms_out[k] = ms / reps;
+        out[k] = ms / reps;
     }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    kernel_bytes(S, mf, out + 4);
+    out[6] = out[7] = 0.0;
     S.iter_ready = false;
 }
 

@@ -13,6 +13,7 @@
 #pragma once
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -34,6 +35,48 @@ struct Sell {
     DBuf<int32_t> ci;   // nent
     DBuf<double> val;   // nent (padding: val 0, col = a valid column of the row)
     DBuf<int32_t> perm; // SELL row -> CSR row (A only; empty = identity).  See build_sell.
+};
+
+// Structured stencil operator (lsq_set_matrix_stencil systems): the constraint rows are never
+// stored — a stencil part is (grid, centre box lo..hi, ≤8 template offsets/values) and row
+// r = row0 + ravel_box(c − lo) of centre c has entries val_t at column col0 + ravel(c + off_t).
+// A·v and Aᵀu walk the grid nodes (one thread per node, all parts of its grid); only the data
+// rows (bi/trilinear interpolation, irregular) stay assembled, as SELL copies Ad / ATd.  The
+// v-space of this operator is the FULL column space [0, n_full): columns removed by the column
+// map (Ip_c) carry column scale 0, so they never enter the iteration (x_j stays 0), which is the
+// same LSQR as on the compacted matrix.
+constexpr int MF_MAX_PARTS = 32, MF_MAX_GRID_PARTS = 16, MF_MAX_GRIDS = 4;
+constexpr int MF_NPT = 4;                    // nodes per thread per block iteration
+constexpr int MF_ALIGN = 256 * MF_NPT;       // node-enumeration alignment of every grid
+constexpr int MF_R = 3;                      // |template offset| <= MF_R (8 edge classes per side)
+struct FastDiv {            // n / d for 0 <= n < 2^31: (n * mul) >> (32 + shift)
+    uint64_t mul;
+    uint32_t shift, d;
+};
+struct MfPart {
+    int32_t grid, ntpl, row0, n_eq;          // rows [row0, row0 + n_eq) (global row ids < 2^31)
+    int32_t lo[3], hi[3], bstride[3];
+    int32_t ilo[3], ihi[3];                  // centres whose every template entry hits the box
+    int32_t off[8][3];
+    int32_t doff[8];                         // column offset of template entry t  (Σ off·stride)
+    int32_t boff[8];                         // row offset of template entry t     (Σ off·bstride)
+    uint64_t mlo[3], mhi[3];                 // template validity masks by edge class (MF_R)
+    int32_t wconst, pad;                     // 1: every row of the part has row scale w
+    double w;
+    double val[8];
+};
+struct MfGrid {
+    int32_t ndim, nparts;
+    int32_t shape[3], col0, nodes, node0;    // node0: first position in the MF_ALIGN-aligned enumeration
+    FastDiv fd[3];
+    int32_t part[MF_MAX_GRID_PARTS];
+};
+struct MfDesc {
+    int32_t n_grids, n_parts;
+    int64_t nodes;                 // end of the node enumeration (grids with parts, MF_ALIGN-aligned)
+    int64_t npts, m, n_full;
+    MfGrid g[MF_MAX_GRIDS];
+    MfPart p[MF_MAX_PARTS];
 };
 
 // LSQR scalar state, device resident (one per handle).  Field meanings follow
@@ -72,6 +115,17 @@ struct System {
     int cs_mode = -1;       // precond the SELL values were filled with (-1 = stale)
     bool rs_dirty = true;
     Sell A, AT;
+    bool sell_built = false;   // A / AT exist (built lazily when the stencil operator is active)
+
+    // structured stencil operator (see MfDesc)
+    bool mf = false;
+    MfDesc mfh{};
+    DBuf<MfDesc> mfd;
+    Sell Ad, ATd;              // data rows (cols = full ids) / their transpose (rows = node-enumeration positions)
+    Csr GdT;                   // transpose of the data rows of G (value source of ATd)
+    DBuf<int32_t> keep;        // compact column -> full column
+    DBuf<double> csf;          // column scale in the full space (0 = removed column)
+    DBuf<double> zv;           // cs ∘ ṽ in the full space (gathered by the stencil rows)
 
     // dense factor (precond 2 / error propagation): R and R⁻¹, npad x npad row-major
     DBuf<double> dR, dRi;
@@ -99,9 +153,11 @@ struct System {
     DBuf<double> part_u, part_v, part_w, part_b;
     DBuf<LsqState> st;
     bool iter_ready = false;   // lsq_iterate state initialised
+    int iter_mode = -1;        // precond * 2 + stencil-operator flag of that state
     int iter_parity = 0;
 
     int64_t ncols_own() const { return dist ? n_own : G.n; }   // columns whose x this rank solves
+    int64_t vlen() const { return mf ? std::max<int64_t>(G.n, n_full) : G.n; }   // workspace v length
     ~System();
 };
 
@@ -125,6 +181,7 @@ void relabel_columns(System& S, const int32_t* h_map, int64_t n_local);
 void form_from_coo(System& S, int64_t m, int64_t n_full, int64_t nnz, const int64_t* r,
                    const int64_t* c, const double* v);
 void finish_formation(System& S);              // G set -> GT, SELL copies, default scaling
+void ensure_sell(System& S);                    // assembled A / AT (lazy when S.mf)
 void refresh_scaling(System& S, int precond);   // rs/cs -> SELL values (single GPU)
 void scaling_rows_colnorm(System& S, int precond, bool raw);
 void scaling_finish_cs(System& S);

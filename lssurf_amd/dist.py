@@ -251,9 +251,9 @@ class DistFitSystem(_Base):
         return st.as_dict()
 
     def info(self):
-        o = np.zeros(6, np.int64)
+        o = np.zeros(8, np.int64)
         self.L.lsq_sell_info(self.h, ptr(o))
-        return dict(zip(['m', 'n', 'nnz', 'sell_A', 'sell_AT', 'device_bytes'], o.tolist()))
+        return dict(zip(['m', 'n', 'nnz', 'sell_A', 'sell_AT', 'device_bytes', 'stencil_op', 'n_full'], o.tolist()))
 
     def close(self):
         if getattr(self, 'h', None):

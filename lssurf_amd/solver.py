@@ -109,35 +109,39 @@ class LSQSolver:
 
     # ---- solve -------------------------------------------------------------------------------
     def solve(self, b, x0=None, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, batch=16,
-              use_graph=True):
+              use_graph=True, op=0):
         """LSQR; returns (x, stats) with scipy-lsqr-style stats (iters, istop, r1norm, ...)."""
         b = as_c(b, np.float64)
         if b.size != self.m:
             raise ValueError(f'b has {b.size} rows, system has {self.m}')
         x = np.zeros(self.n) if x0 is None else as_c(x0, np.float64).copy()
         o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond),
-                         use_x0=int(x0 is not None), batch=int(batch), use_graph=int(bool(use_graph)))
+                         use_x0=int(x0 is not None), batch=int(batch), use_graph=int(bool(use_graph)), op=int(op))
         st = LsqStats()
         self._check(self._L.lsq_solve(self._h, ptr(b), ptr(x), ctypes.byref(o), ctypes.byref(st)), 'lsq_solve')
         return x, st.as_dict()
 
-    def iterate(self, b, iters, precond=1, batch=16, use_graph=True):
+    def iterate(self, b, iters, precond=1, batch=16, use_graph=True, op=0):
         b = as_c(b, np.float64)
-        o = default_opts(precond=int(precond), batch=int(batch), use_graph=int(bool(use_graph)))
+        o = default_opts(precond=int(precond), batch=int(batch), use_graph=int(bool(use_graph)), op=int(op))
         st = LsqStats()
         self._check(self._L.lsq_iterate(self._h, ptr(b), int(iters), ctypes.byref(o), ctypes.byref(st)),
                     'lsq_iterate')
         return st.as_dict()
 
-    def profile_kernels(self, reps=20):
-        ms = np.zeros(4)
-        self._check(self._L.lsq_profile_kernels(self._h, int(reps), ptr(ms)), 'lsq_profile_kernels')
-        return dict(zip(['xw_spmv', 'spmtv', 'beta', 'givens'], ms.tolist()))
+    def profile_kernels(self, reps=20, op=0):
+        """Per-kernel device time (ms) of one iteration's launches of operator `op`, and the
+        algorithmic HBM bytes per launch of the two streaming kernels."""
+        o = np.zeros(8)
+        self._check(self._L.lsq_profile_kernels(self._h, int(reps), int(op), ptr(o)), 'lsq_profile_kernels')
+        d = dict(zip(['xw_spmv', 'spmtv', 'beta', 'givens'], o[:4].tolist()))
+        d['bytes'] = {'xw_spmv': float(o[4]), 'spmtv': float(o[5])}
+        return d
 
     def info(self):
-        o = np.zeros(6, np.int64)
+        o = np.zeros(8, np.int64)
         self._check(self._L.lsq_sell_info(self._h, ptr(o)), 'lsq_sell_info')
-        return dict(zip(['m', 'n', 'nnz', 'sell_A', 'sell_AT', 'device_bytes'], o.tolist()))
+        return dict(zip(['m', 'n', 'nnz', 'sell_A', 'sell_AT', 'device_bytes', 'stencil_op', 'n_full'], o.tolist()))
 
     def sigma_x(self):
         """sqrt(diag((AᵀA)⁻¹)) of the current weighted, masked system (dense device Cholesky)."""

@@ -253,3 +253,51 @@ def test_stencil_formation_equals_coo_formation_t64(gpu_available):
     np.testing.assert_array_equal(a.indptr, b.indptr)
     np.testing.assert_array_equal(a.indices, b.indices)
     np.testing.assert_array_equal(a.data, b.data)
+
+
+def _t64_system():
+    from lssurf_amd import synthetic
+    D, kw = synthetic.points('t64')
+    S = LS.smooth_fit(data=D, return_fit_objects=True, VERBOSE=False, **kw)
+    keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch'])
+    fs = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N)
+    E_all = 1 / (1. / np.concatenate((S['Ed'], S['Ec'])))
+    w = 1. / np.sqrt(E_all ** 2)
+    rhs = np.zeros(w.size)
+    rhs[:S['data'].size] = S['data'].z
+    return S, fs, w, rhs
+
+
+def test_stencil_operator_equals_assembled_operator(gpu_available):
+    """The structured stencil operator (op 0) and the assembled SELL operator (op 1) run the same
+    LSQR: after 40 fixed iterations the recurrence scalars agree to rounding, converged solutions
+    to the solver tolerance."""
+    S, fs, w, rhs = _t64_system()
+    try:
+        assert fs.solver.info()['stencil_op'] == 1
+        fs.solver.set_row_weight(w)
+        stats = [fs.solver.iterate(rhs, 40, op=op) for op in (0, 1)]
+        for k in ('r1norm', 'anorm', 'arnorm', 'xnorm', 'acond'):
+            assert abs(stats[0][k] - stats[1][k]) <= 1e-9 * abs(stats[1][k]), (k, stats)
+        xs = [fs.solver.solve(rhs, atol=1e-12, btol=1e-12, conlim=1e12, op=op)[0] for op in (0, 1)]
+    finally:
+        fs.close()
+    assert np.linalg.norm(xs[0] - xs[1]) / np.linalg.norm(xs[1]) <= 1e-8
+
+
+def test_stencil_operator_mask_reweight_warm_start(gpu_available):
+    S, fs, w, rhs = _t64_system()
+    rng = np.random.default_rng(3)
+    keep = rng.random(fs.n_data) > 0.1
+    w2 = w * np.where(np.arange(w.size) < fs.n_data, rng.uniform(0.5, 2, w.size), 1.0)
+    try:
+        x0 = fs.solve(w2, keep, rhs, atol=1e-12, btol=1e-12, conlim=1e12, op=1)
+        x1 = fs.solve(w2, keep, rhs, atol=1e-12, btol=1e-12, conlim=1e12, op=0)
+        it_cold = fs.stats['iters']
+        x2 = fs.solve(w2, keep, rhs, x0=x1, atol=1e-12, btol=1e-12, conlim=1e12, op=0)
+        it_warm = fs.stats['iters']
+    finally:
+        fs.close()
+    assert np.linalg.norm(x1 - x0) / np.linalg.norm(x0) <= 1e-8
+    assert np.linalg.norm(x2 - x0) / np.linalg.norm(x0) <= 1e-8
+    assert it_warm < it_cold
