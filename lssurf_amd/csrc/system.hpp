@@ -46,7 +46,7 @@ struct Sell {
 // map (Ip_c) carry column scale 0, so they never enter the iteration (x_j stays 0), which is the
 // same LSQR as on the compacted matrix.
 constexpr int MF_MAX_PARTS = 32, MF_MAX_GRID_PARTS = 16, MF_MAX_GRIDS = 4;
-constexpr int MF_NPT = 4;                    // nodes per thread per block iteration
+constexpr int MF_NPT = 2;                    // nodes per thread per block iteration
 constexpr int MF_ALIGN = 256 * MF_NPT;       // node-enumeration alignment of every grid
 constexpr int MF_R = 3;                      // |template offset| <= MF_R (8 edge classes per side)
 struct FastDiv {            // n / d for 0 <= n < 2^31: (n * mul) >> (32 + shift)
