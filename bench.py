@@ -39,7 +39,7 @@ def build_system(config, device):
     S = LS.smooth_fit(data=D, return_fit_objects=True, VERBOSE=False, **kw)
     keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch'])
     t1 = time.time()
-    fs = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, device=device)
+    fs = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, device=device, grids=S['grids'])
     E_all = 1 / (1. / np.concatenate((S['Ed'], S['Ec'])))
     w = 1. / np.sqrt(E_all ** 2)
     rhs = np.zeros(w.size)
@@ -82,10 +82,10 @@ class _Dist:
     def info(self):
         return self.ds.info()
 
-    def iterate(self, rhs, iters, op=0):
+    def iterate(self, rhs, iters, op=0, precond=1):
         return self.ds.iterate(None, None, iters)
 
-    def solve(self, rhs, op=0):
+    def solve(self, rhs, op=0, precond=1):
         x = self.ds.solve(None, None)
         return x, self.ds.stats
 
@@ -174,6 +174,8 @@ def main():
     ap.add_argument('--dist', action='store_true', help='use the distributed (RCCL) path even at N=1')
     ap.add_argument('--no-pmc', action='store_true', help='skip the rocprofv3 PMC traffic passes')
     ap.add_argument('--op', type=int, default=0, help='0: auto (structured stencil operator), 1: assembled SELL')
+    ap.add_argument('--precond', type=int, default=1,
+                    help='1: column scaling, 3: block-Jacobi per (y,x) node (single GPU)')
     ap.add_argument('--pmc-child', action='store_true', help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
@@ -204,10 +206,10 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    solver.iterate(rhs, args.warmup, op=args.op)
+    solver.iterate(rhs, args.warmup, op=args.op, precond=args.precond)
     barrier()
     t0 = time.perf_counter()
-    st = solver.iterate(rhs, args.steps, op=args.op)   # synchronous: returns after the device finished
+    st = solver.iterate(rhs, args.steps, op=args.op, precond=args.precond)   # synchronous: returns after the device finished
     barrier()
     t_wall = time.perf_counter() - t0
     t_dev = st['time_s']
@@ -238,8 +240,13 @@ def main():
 
     solve = {}
     if not args.no_solve:
-        x, sst = solver.solve(rhs, op=args.op)
+        x, sst = solver.solve(rhs, op=args.op, precond=args.precond)
         solve = {'solve_time_s': sst['time_s'], 'solve_iters': int(sst['iters']), 'solve_istop': int(sst['istop'])}
+        if args.precond != 3 and getattr(fs, 'has_blocks', False):   # smooth_fit's default for large n
+            x3, s3 = solver.solve(rhs, op=args.op, precond=3)
+            solve['block_jacobi'] = {'solve_time_s': s3['time_s'], 'solve_iters': int(s3['iters']),
+                                     'solve_istop': int(s3['istop']),
+                                     'rel_diff_vs_jacobi': float(np.linalg.norm(x3 - x) / np.linalg.norm(x))}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not args.dist:
@@ -257,7 +264,7 @@ def main():
             'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f64',
             'data': 'synthetic (SURVEY.md §8(d) point cloud)',
             'config': {'workload': f'smooth_fit LSQR, {args.config}', 'rank0_system': info, 'rows': gm, 'cols': gn,
-                       'nnz': gZ, 'precond': 'column scaling',
+                       'nnz': gZ, 'precond': {1: 'column scaling', 3: 'block-Jacobi per (y,x) node'}.get(args.precond, args.precond),
                        'operator': 'structured stencil rows + SELL data rows' if info.get('stencil_op') and args.op == 0
                        and not isinstance(solver, _Dist) else 'assembled SELL',
                        'parallelism': f'y-slab rows x{world} (RCCL)' if world > 1 or args.dist else 'single'},

@@ -44,7 +44,9 @@ typedef struct lsq_handle lsq_handle;
 typedef struct lsq_opts {
     int32_t method;        /* 0 = LSQR (Paige & Saunders 1982)                                 */
     int32_t precond;       /* 0 = none, 1 = column (Jacobi) scaling, 2 = dense Cholesky R⁻¹   */
-                           /*     (exact right preconditioner; n up to a few 10^4)             */
+                           /*     (exact right preconditioner; n up to a few 10^4), 3 = block-  */
+                           /*     Jacobi: R_b⁻¹ of every column block (lsq_set_column_blocks;   */
+                           /*     SURVEY.md §8 a7.4 — no reference counterpart)                 */
     double  atol, btol, conlim;
     int64_t maxit;
     int32_t use_x0;        /* 1: x_inout holds a warm start (outer-iteration "resume")          */
@@ -120,6 +122,13 @@ int lsq_set_row_weight(lsq_handle* h, const double* row_weight);
 /* Row selection Ip_r (smooth_fit.py:132-135): rows with keep[i] == 0 are excluded from the
  * fit (treated as absent rows).  NULL keeps every row. */
 int lsq_set_row_mask(lsq_handle* h, const uint8_t* keep);
+/* Column blocks of the block-Jacobi preconditioner (precond 3): block b holds the compact
+ * columns cols[block_ptr[b] .. block_ptr[b+1]) (at most 16, each column in at most one block);
+ * unlisted columns are singleton blocks.  For smooth_fit a block is one (y, x) node: its z0
+ * column and its dz columns of every kept epoch.  The factors R_b (AᵀA restricted to the block
+ * = R_bᵀR_b, with the current row weights / mask) are rebuilt on the device when weights change.
+ * NULL / 0 blocks clears the structure (every column its own block). */
+int lsq_set_column_blocks(lsq_handle* h, int64_t n_blocks, const int64_t* block_ptr, const int32_t* cols);
 
 int lsq_shape(lsq_handle* h, int64_t* m, int64_t* n, int64_t* nnz);
 /* Download the formed A (selected rows only, in row order; canonical CSR, sorted columns). */

@@ -43,7 +43,8 @@ class LsqStats(ctypes.Structure):
 
 # every symbol declared in include/lsqsurf.h
 EXPORTS = ['lsq_default_opts', 'lsq_create', 'lsq_destroy', 'lsq_last_error', 'lsq_set_col_map',
-           'lsq_set_matrix_coo', 'lsq_set_matrix_stencil', 'lsq_set_row_weight', 'lsq_set_row_mask', 'lsq_shape', 'lsq_get_csr',
+           'lsq_set_matrix_coo', 'lsq_set_matrix_stencil', 'lsq_set_row_weight', 'lsq_set_row_mask',
+           'lsq_set_column_blocks', 'lsq_shape', 'lsq_get_csr',
            'lsq_solve', 'lsq_spmv', 'lsq_iterate', 'lsq_profile_kernels', 'lsq_sell_info', 'lsq_sigma_x',
            'lsq_get_rinv', 'lsq_dist_unique_id', 'lsq_create_dist', 'lsq_dist_referenced_cols',
            'lsq_dist_set_layout', 'lsq_vgroup_create', 'lsq_vgroup_rank', 'lsq_vgroup_solve', 'lsq_vgroup_iterate',
@@ -72,6 +73,7 @@ def load():
         'lsq_set_row_weight': ([P, P], ctypes.c_int),
         'lsq_set_matrix_stencil': ([P, i64, i64, i32, P, i32, P, i64, P, P, P, i32, P, P], ctypes.c_int),
         'lsq_set_row_mask': ([P, P], ctypes.c_int),
+        'lsq_set_column_blocks': ([P, i64, P, P], ctypes.c_int),
         'lsq_shape': ([P, P, P, P], ctypes.c_int),
         'lsq_get_csr': ([P, P, P, P], ctypes.c_int),
         'lsq_solve': ([P, P, P, P, P], ctypes.c_int),

@@ -86,3 +86,50 @@ def build_reference_epoch_matrix(G_data, Gc, grids, reference_epoch, dz_mask=Non
         raise NotImplementedError('build_reference_epoch_matrix: dz_mask is outside lssurf_amd')
     keep = reference_epoch_keep_cols(G_data.col_N, grids['dz'], reference_epoch)
     return sp.coo_matrix((np.ones_like(keep), (keep, np.arange(keep.size))), shape=(Gc.col_N, keep.size)).tocsc()
+
+
+def node_column_blocks(grids, keep_cols, max_block=16):
+    """Column blocks of the block-Jacobi preconditioner (lsq precond 3):
+    one block per (y, x) node = its z0 column (when the z0 and dz grids share the node lattice)
+    and its dz columns of every kept epoch, in compact column ids (`keep_cols` ascending, as
+    returned by reference_epoch_keep_cols).  Blocks longer than `max_block` are split along t.
+    Returns (block_ptr, cols) or None when the grids do not have that structure."""
+    z0, dz = grids.get('z0'), grids.get('dz')
+    if dz is None or dz.N_dims != 3:
+        return None
+    keep_cols = np.asarray(keep_cols)
+    ny, nx, nt = (int(s) for s in dz.shape)
+    nodes = np.arange(ny * nx)
+    dz_cols = dz.col_0 + nodes[:, None] * nt + np.arange(nt)[None, :]          # (nodes, nt) full ids
+    same = z0 is not None and tuple(z0.shape) == (ny, nx) and all(
+        np.array_equal(a, b) for a, b in zip(z0.ctrs, dz.ctrs[:2]))
+    parts = [(z0.col_0 + nodes)[:, None]] if same else []
+    full = np.concatenate(parts + [dz_cols], axis=1)                           # (nodes, k)
+    pos = np.searchsorted(keep_cols, full)
+    pos_c = np.minimum(pos, keep_cols.size - 1)
+    kept = keep_cols[pos_c] == full
+    cols, lens = [], []
+    k_all = kept.sum(axis=1)
+    if np.all(k_all == k_all[0]):                 # the usual case: same kept set at every node
+        k = int(k_all[0])
+        comp = pos_c[kept].reshape(-1, k)
+        nsplit = -(-k // max_block)
+        for s in range(nsplit):
+            sl = comp[:, s * max_block:(s + 1) * max_block]
+            cols.append(sl)
+            lens.append(np.full(sl.shape[0], sl.shape[1]))
+        order = np.argsort(np.concatenate([np.arange(ny * nx) * nsplit + s for s in range(nsplit)]), kind='stable')
+        lens = np.concatenate(lens)[order]
+        flat = np.concatenate([c.reshape(-1, c.shape[1]) for c in cols]) if nsplit == 1 else None
+        if nsplit == 1:
+            cols = flat.ravel()
+        else:
+            rows = [list(c) for c in cols]
+            cols = np.concatenate([np.concatenate([rows[s][i] for s in range(nsplit)]) for i in range(ny * nx)])
+    else:
+        out = [pos_c[i][kept[i]] for i in range(ny * nx)]
+        chunks = [o[s:s + max_block] for o in out for s in range(0, max(len(o), 1), max_block) if len(o)]
+        lens = np.array([len(c) for c in chunks])
+        cols = np.concatenate(chunks)
+    ptr = np.r_[0, np.cumsum(lens)].astype(np.int64)
+    return ptr, np.asarray(cols, dtype=np.int32)

@@ -167,6 +167,16 @@ int lsq_set_row_weight(lsq_handle* h, const double* row_weight) {
     });
 }
 
+int lsq_set_column_blocks(lsq_handle* h, int64_t n_blocks, const int64_t* block_ptr, const int32_t* cols) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_set_column_blocks: no matrix");
+        if (S.dist) return fail(S, "lsq_set_column_blocks: single-GPU handles only");
+        lsq::graph_cache_drop(&S);
+        lsq::set_column_blocks(S, n_blocks > 0 ? n_blocks : 0, block_ptr, cols);
+        return 0;
+    });
+}
+
 int lsq_set_row_mask(lsq_handle* h, const uint8_t* keep) {
     return guarded(h, [&](lsq::System& S) {
         if (!S.G.rp.p) return fail(S, "lsq_set_row_mask: no matrix");
@@ -238,7 +248,7 @@ int lsq_solve(lsq_handle* h, const double* b, double* x_inout, const lsq_opts* o
         lsq_default_opts(&d);
         if (!o) o = &d;
         if (o->method != 0) return fail(S, "lsq_solve: only method 0 (LSQR) is implemented");
-        if (o->precond < 0 || o->precond > 2) return fail(S, "lsq_solve: precond must be 0, 1 or 2");
+        if (o->precond < 0 || o->precond > 3) return fail(S, "lsq_solve: precond must be 0, 1, 2 or 3");
         if (S.dist) {
             if (S.virt) return fail(S, "lsq_solve: a virtual rank solves through lsq_vgroup_solve");
             lsq::Group G;

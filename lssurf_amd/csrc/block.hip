@@ -1,0 +1,176 @@
+// block.hip — block-Jacobi preconditioner (precond 3; SURVEY.md §8 a7.4 — the reference solves
+// directly with SuiteSparseQR and has no counterpart).
+//
+// Right preconditioner M = blockdiag(R_b⁻¹) with R_bᵀR_b = (AᵀA)_bb, A = diag(rs)·G: LSQR runs on
+// A·M, whose column blocks are orthonormal in the block's own metric.  For smooth_fit a block is
+// one (y, x) node — its z0 column and the dz columns of every kept epoch — so the strong
+// z0/dz/epoch coupling of the data rows and the time-derivative constraints is removed exactly;
+// the iteration count then depends on the spatial coupling only.
+//
+// Factorisation: one thread per block.  (AᵀA)_bb entries are merges of two sorted GT rows
+// (deterministic, no atomics), then an in-register Cholesky and triangular inverse.  Columns
+// whose pivot vanishes (empty or dependent inside the block) are dropped: their rows and columns
+// of R_b⁻¹ are zero, so the iteration never moves them (x_j = 0).
+#include <algorithm>
+#include <vector>
+
+#include "system.hpp"
+
+namespace lsq {
+namespace {
+
+constexpr int KB = 16;                     // maximum block size
+constexpr int KB_PACK = KB * (KB + 1) / 2;
+
+__device__ __forceinline__ int pk(int i, int j) { return j * (j + 1) / 2 + i; }   // i <= j
+
+// Σ_r rs_r² · G_ri · G_rj over the common rows of GT rows a and b (ascending row ids)
+__device__ double col_dot(const int64_t* __restrict__ trp, const int32_t* __restrict__ tci,
+                          const double* __restrict__ tval, const double* __restrict__ rs, int32_t a, int32_t b) {
+    int64_t p = trp[a], pe = trp[a + 1], q = trp[b], qe = trp[b + 1];
+    double s = 0.0;
+    while (p < pe && q < qe) {
+        const int32_t rp = tci[p], rq = tci[q];
+        if (rp == rq) {
+            const double w = rs[rp];
+            s += (w * tval[p]) * (w * tval[q]);
+            ++p;
+            ++q;
+        } else if (rp < rq) {
+            ++p;
+        } else {
+            ++q;
+        }
+    }
+    return s;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_block_factor(int64_t nb, const int64_t* __restrict__ ptr,
+                                                        const int32_t* __restrict__ cols,
+                                                        const int64_t* __restrict__ trp,
+                                                        const int32_t* __restrict__ tci,
+                                                        const double* __restrict__ tval,
+                                                        const double* __restrict__ rs, int kmax,
+                                                        double* __restrict__ Ri, unsigned long long* ndead) {
+    const int npk = kmax * (kmax + 1) / 2;
+    for (int64_t b = (int64_t)blockIdx.x * BLOCK + threadIdx.x; b < nb; b += (int64_t)gridDim.x * BLOCK) {
+        const int64_t b0 = ptr[b];
+        const int k = (int)(ptr[b + 1] - b0);
+        int32_t c[KB];
+        for (int i = 0; i < k; ++i) c[i] = cols[b0 + i];
+        double R[KB_PACK];   // N, then R in place (upper, packed by columns)
+        double d0[KB];
+        for (int j = 0; j < k; ++j)
+            for (int i = 0; i <= j; ++i) R[pk(i, j)] = col_dot(trp, tci, tval, rs, c[i], c[j]);
+        for (int j = 0; j < k; ++j) d0[j] = R[pk(j, j)];
+        bool dead[KB];
+        // Cholesky by columns: R_ij = (N_ij − Σ_{l<i} R_li R_lj) / R_ii, R_jj = sqrt(N_jj − Σ R_lj²)
+        for (int j = 0; j < k; ++j) {
+            for (int i = 0; i < j; ++i) {
+                if (dead[i]) {
+                    R[pk(i, j)] = 0.0;
+                    continue;
+                }
+                double s = R[pk(i, j)];
+                for (int l = 0; l < i; ++l) s -= R[pk(l, i)] * R[pk(l, j)];
+                R[pk(i, j)] = s / R[pk(i, i)];
+            }
+            double d = R[pk(j, j)];
+            for (int l = 0; l < j; ++l) d -= R[pk(l, j)] * R[pk(l, j)];
+            dead[j] = !(d > 1e-12 * d0[j]) || !(d0[j] > 0.0);
+            if (dead[j]) {
+                for (int l = 0; l < j; ++l) R[pk(l, j)] = 0.0;
+                R[pk(j, j)] = 1.0;
+                atomicAdd(ndead, 1ull);
+            } else {
+                R[pk(j, j)] = sqrt(d);
+            }
+        }
+        // R⁻¹ (upper) in place, column by column from the diagonal up
+        double X[KB_PACK];
+        for (int j = 0; j < k; ++j) {
+            X[pk(j, j)] = 1.0 / R[pk(j, j)];
+            for (int i = j - 1; i >= 0; --i) {
+                double s = 0.0;
+                for (int l = i + 1; l <= j; ++l) s += R[pk(i, l)] * X[pk(l, j)];
+                X[pk(i, j)] = -s / R[pk(i, i)];
+            }
+        }
+        for (int j = 0; j < k; ++j)
+            for (int i = 0; i <= j; ++i)
+                if (dead[i] || dead[j]) X[pk(i, j)] = 0.0;
+        for (int e = 0; e < npk; ++e) Ri[(int64_t)e * nb + b] = e < k * (k + 1) / 2 ? X[e] : 0.0;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_full_ids(int64_t n, const int32_t* __restrict__ cols,
+                                                    const int32_t* __restrict__ keep, int32_t* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK)
+        out[i] = keep ? keep[cols[i]] : cols[i];
+}
+
+}  // namespace
+
+void set_column_blocks(System& S, int64_t nb, const int64_t* ptr, const int32_t* cols) {
+    const int64_t n = S.G.n;
+    std::vector<int64_t> P;
+    std::vector<int32_t> C;
+    std::vector<uint8_t> seen(n, 0);
+    P.push_back(0);
+    int kmax = 1;
+    if (nb > 0) {
+        if (!ptr || !cols || ptr[0] != 0) throw std::invalid_argument("lsq_set_column_blocks: bad block_ptr");
+        for (int64_t b = 0; b < nb; ++b) {
+            const int64_t k = ptr[b + 1] - ptr[b];
+            if (k < 1 || k > KB) throw std::invalid_argument("lsq_set_column_blocks: block size must be 1..16");
+            for (int64_t e = ptr[b]; e < ptr[b + 1]; ++e) {
+                const int32_t c = cols[e];
+                if (c < 0 || c >= n) throw std::invalid_argument("lsq_set_column_blocks: column out of range");
+                if (seen[c]) throw std::invalid_argument("lsq_set_column_blocks: column in two blocks");
+                seen[c] = 1;
+                C.push_back(c);
+            }
+            P.push_back((int64_t)C.size());
+            kmax = std::max<int>(kmax, (int)k);
+        }
+    }
+    for (int64_t c = 0; c < n; ++c)   // the rest: singletons
+        if (!seen[c]) {
+            C.push_back((int32_t)c);
+            P.push_back((int64_t)C.size());
+        }
+    S.nblk = (int64_t)P.size() - 1;
+    S.blk_kmax = kmax;
+    S.blk_ptr.alloc(S.nblk + 1);
+    S.blk_ptr.upload(P.data(), S.nblk + 1, S.stream);
+    S.blk_cols.alloc(std::max<int64_t>((int64_t)C.size(), 1));
+    S.blk_cols.upload(C.data(), (int64_t)C.size(), S.stream);
+    S.blk_full.alloc(std::max<int64_t>((int64_t)C.size(), 1));
+    hipLaunchKernelGGL(k_full_ids, dim3(grid_for((int64_t)C.size())), dim3(BLOCK), 0, S.stream, (int64_t)C.size(),
+                       S.blk_cols.p, S.mf ? S.keep.p : nullptr, S.blk_full.p);
+    KERNEL_CHECK();
+    S.blk_Ri = DBuf<double>();
+    S.blk_valid = false;
+    S.blk_user = nb > 0;
+    S.iter_ready = false;
+    HIP_CHECK(hipStreamSynchronize(S.stream));
+}
+
+void ensure_blocks(System& S) {
+    if (S.nblk == 0) set_column_blocks(S, 0, nullptr, nullptr);
+}
+
+void block_factor(System& S) {
+    ensure_blocks(S);
+    const int npk = S.blk_kmax * (S.blk_kmax + 1) / 2;
+    if (S.blk_Ri.n != (int64_t)npk * S.nblk) S.blk_Ri.alloc((int64_t)npk * S.nblk);
+    DBuf<unsigned long long> nd(1);
+    nd.zero(S.stream);
+    hipLaunchKernelGGL(k_block_factor, dim3(grid_for(S.nblk)), dim3(BLOCK), 0, S.stream, S.nblk, S.blk_ptr.p,
+                       S.blk_cols.p, S.GT.rp.p, S.GT.ci.p, S.GT.val.p, S.rs.p, S.blk_kmax, S.blk_Ri.p, nd.p);
+    KERNEL_CHECK();
+    HIP_CHECK(hipStreamSynchronize(S.stream));
+    S.blk_valid = true;
+}
+
+}  // namespace lsq

@@ -622,6 +622,9 @@ void finish_formation(System& S) {
     S.rs_dirty = true;
     S.cs_mode = -1;
     S.iter_ready = false;
+    S.nblk = 0;   // column blocks refer to the previous column numbering
+    S.blk_user = false;
+    S.blk_valid = false;
     HIP_CHECK(hipStreamSynchronize(st));
 }
 
@@ -633,7 +636,8 @@ void scaling_rows_colnorm(System& S, int precond, bool raw) {
     const int64_t m = S.G.m, n = S.G.n;
     hipLaunchKernelGGL(k_rowscale, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, S.roww.p, S.rowkeep.p, S.rs.p);
     KERNEL_CHECK();
-    S.dense_valid = false;   // the dense factor depends on the row scaling
+    S.dense_valid = false;   // the dense and block factors depend on the row scaling
+    S.blk_valid = false;
     if (precond == 1)
         hipLaunchKernelGGL(k_colnorm, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, S.GT.rp.p, S.GT.ci.p, S.GT.val.p,
                            S.rs.p, S.cs.p, raw ? 1 : 0);

@@ -359,15 +359,18 @@ __global__ __launch_bounds__(BLOCK) void k_scatter_add(int64_t cnt, const int32_
 }
 
 #include "lsqr_mf.inc"
+#include "lsqr_block.inc"
 
 struct Grids {
     int gA, gT, gX, gR, gRT, gE;
     int gD, gS, gM, gXf;   // stencil operator: data-row blocks, node blocks, Aᵀu blocks, x/w blocks
+    int gB;                // block-Jacobi epilogue
 };
 
 Grids grids_for(const System& S) {
     Grids g;
     g.gD = g.gS = g.gM = g.gXf = 1;
+    g.gB = grid_for(std::max<int64_t>(S.nblk, 1), BLOCK, NPART);
     if (S.mf) {
         g.gD = (int)std::min<int64_t>(std::max<int64_t>((S.Ad.nslices + 3) / 4, 1), NPART / 4);
         g.gS = (int)std::min<int64_t>(std::max<int64_t>(S.mfh.nodes / MF_ALIGN, 1), NPART - g.gD);
@@ -411,15 +414,21 @@ void launch_iteration(System& S, const Grids& g, int p, int precond) {
     hipStream_t st = S.stream;
     double* vt = p ? S.vb1.p : S.vb0.p;
     double* vo = p ? S.vb0.p : S.vb1.p;
-    const bool dense = precond == 2;
+    const bool dense = precond == 2, block = precond == 3;
     if (dense)   // z = R⁻¹ ṽ / α
         hipLaunchKernelGGL(k_gemv_upper, dim3(g.gR), dim3(BLOCK), 0, st, S.dRi.p, S.G.n, S.dense_ld, vt, S.st.p, 1,
                            S.zt.p);
+    // gathered vector: ṽ (values carry cs), R⁻¹ṽ/α (dense), or z = M ṽ from the block epilogue
     hipLaunchKernelGGL(k_xw_spmv, dim3(g.gX + g.gA), dim3(BLOCK), 0, st, S.st.p, g.gX, S.G.n, S.y.p, S.w.p, vt,
-                       dense ? S.zt.p : vt, dense ? 0 : 1, S.G.m, S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p, S.u.p,
-                       S.part_u.p, S.part_w.p);
+                       (dense || block) ? S.zt.p : vt, dense ? 0 : 1, S.G.m, S.A.nslices, S.A.sp.p, S.A.ci.p,
+                       S.A.val.p, S.u.p, S.part_u.p, S.part_w.p);
     hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gA, S.part_b.p, 0, 0, nullptr);
-    if (dense) {
+    if (block) {
+        hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, S.G.n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
+                           S.AT.val.p, S.u.p, vt, S.tt.p, S.part_v.p, 1);
+        launch_block_epi(S, false, g.gB, S.tt.p, vt, vo, S.zt.p);
+        hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gB, S.part_w.p, g.gX, 0, nullptr);
+    } else if (dense) {
         hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, S.G.n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
                            S.AT.val.p, S.u.p, vt, S.tt.p, S.part_v.p, 1);
         hipLaunchKernelGGL(k_gemvT_upper, dim3(g.gRT), dim3(BLOCK), 0, st, S.dRi.p, S.G.n, S.dense_ld, S.tt.p, S.st.p,
@@ -433,7 +442,7 @@ void launch_iteration(System& S, const Grids& g, int p, int precond) {
 }
 
 // one iteration on the structured stencil operator (full column space, zv = cs∘ṽ)
-void launch_iteration_mf(System& S, const Grids& g, int p) {
+void launch_iteration_mf(System& S, const Grids& g, int p, int precond) {
     hipStream_t st = S.stream;
     double* vt = p ? S.vb1.p : S.vb0.p;
     double* vo = p ? S.vb0.p : S.vb1.p;
@@ -442,8 +451,16 @@ void launch_iteration_mf(System& S, const Grids& g, int p) {
                        S.u.p, S.part_u.p, S.part_w.p);
     hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gD + g.gS, S.part_b.p, 0, 0,
                        nullptr);
+    if (precond == 3) {   // raw Aᵀũ, then ṽ' = M^T t/β − βṽ/α and zv = M ṽ' per column block
+        hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.sp.p, S.ATd.ci.p, S.ATd.val.p,
+                           S.mfd.p, S.u.p, S.rs.p, S.csf.p, vt, S.tt.p, S.zv.p, S.part_v.p, 1);
+        launch_block_epi(S, true, g.gB, S.tt.p, vt, vo, S.zv.p);
+        hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gB, S.part_w.p, g.gXf, 0,
+                           nullptr);
+        return;
+    }
     hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.sp.p, S.ATd.ci.p, S.ATd.val.p,
-                       S.mfd.p, S.u.p, S.rs.p, S.csf.p, vt, vo, S.zv.p, S.part_v.p);
+                       S.mfd.p, S.u.p, S.rs.p, S.csf.p, vt, vo, S.zv.p, S.part_v.p, 0);
     hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gM, S.part_w.p, g.gXf, 0, nullptr);
 }
 
@@ -488,7 +505,12 @@ void lsqr_init_mf(System& S, const double* h_b, const double* h_x0, const lsq_op
         dz0.alloc(std::max<int64_t>(nf, 1));
         dy0.zero(st);
         dz0.zero(st);
-        hipLaunchKernelGGL(k_mf_warm, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, S.keep.p, dx0.p, S.cs.p, dy0.p, dz0.p);
+        if (o.precond == 3)   // y0 = M⁻¹ x0 per block, z0 = x0 (full space)
+            hipLaunchKernelGGL(k_block_warm, dim3(grid_for(S.nblk)), dim3(BLOCK), 0, st, S.nblk, S.blk_ptr.p,
+                               S.blk_cols.p, S.blk_full.p, S.blk_Ri.p, dx0.p, dy0.p, dz0.p);
+        else
+            hipLaunchKernelGGL(k_mf_warm, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, S.keep.p, dx0.p, S.cs.p, dy0.p,
+                               dz0.p);
         KERNEL_CHECK();
     }
     LsqState h{};
@@ -506,9 +528,20 @@ void lsqr_init_mf(System& S, const double* h_b, const double* h_x0, const lsq_op
     hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gD + g.gS, S.part_b.p,
                        g.gD + g.gS, 1, nullptr);
     S.vb1.zero(st);
-    hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.sp.p, S.ATd.ci.p, S.ATd.val.p,
-                       S.mfd.p, S.u.p, S.rs.p, S.csf.p, S.vb1.p, S.vb0.p, S.zv.p, S.part_v.p);
-    hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gM, S.part_w.p, g.gXf, 1, nullptr);
+    if (o.precond == 3) {
+        S.vb0.zero(st);   // columns outside every block (removed by Ip_c) stay 0
+        S.zv.zero(st);
+        hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.sp.p, S.ATd.ci.p, S.ATd.val.p,
+                           S.mfd.p, S.u.p, S.rs.p, S.csf.p, S.vb1.p, S.tt.p, S.zv.p, S.part_v.p, 1);
+        launch_block_epi(S, true, g.gB, S.tt.p, S.vb1.p, S.vb0.p, S.zv.p);
+        hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gB, S.part_w.p, g.gXf, 1,
+                           nullptr);
+    } else {
+        hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.sp.p, S.ATd.ci.p, S.ATd.val.p,
+                           S.mfd.p, S.u.p, S.rs.p, S.csf.p, S.vb1.p, S.vb0.p, S.zv.p, S.part_v.p, 0);
+        hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gM, S.part_w.p, g.gXf, 1,
+                           nullptr);
+    }
     hipLaunchKernelGGL(k_init_w, dim3(g.gXf), dim3(BLOCK), 0, st, S.st.p, nf, S.vb0.p, h_x0 ? dy0.p : nullptr, S.w.p,
                        S.y.p, S.part_w.p);
     KERNEL_CHECK();
@@ -524,7 +557,7 @@ void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts&
     ensure_workspace(S);
     const Grids g = grids_for(S);
     const int64_t m = S.G.m, n = S.G.n;
-    const bool dense = o.precond == 2;
+    const bool dense = o.precond == 2, block = o.precond == 3;
     DBuf<double> db(std::max<int64_t>(m, 1));
     db.upload(h_b, m, st);
     DBuf<double> dx0, dy0;
@@ -532,7 +565,10 @@ void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts&
         dx0.alloc(std::max<int64_t>(n, 1));
         dy0.alloc(std::max<int64_t>(n, 1));
         dx0.upload(h_x0, n, st);
-        if (dense) {   // y0 = R x0 ; the SELL values are unscaled, so A·M·y0 = A x0
+        if (block) {   // y0 = M⁻¹ x0 per block; the SELL values are unscaled, so A·M·y0 = A x0
+            hipLaunchKernelGGL(k_block_warm, dim3(grid_for(S.nblk)), dim3(BLOCK), 0, st, S.nblk, S.blk_ptr.p,
+                               S.blk_cols.p, S.blk_cols.p, S.blk_Ri.p, dx0.p, dy0.p, S.zt.p);
+        } else if (dense) {   // y0 = R x0 ; the SELL values are unscaled, so A·M·y0 = A x0
             hipLaunchKernelGGL(k_gemv_upper, dim3(g.gR), dim3(BLOCK), 0, st, S.dR.p, n, S.dense_ld, dx0.p, nullptr, 2,
                                dy0.p);
         } else {       // y0 = x0 / cs ; A·D·y0 = A x0 with the scaled SELL values
@@ -548,8 +584,8 @@ void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts&
     h.no_stop = no_stop ? 1 : 0;
     h.cs2 = -1.0;
     HIP_CHECK(hipMemcpyAsync(S.st.p, &h, sizeof(h), hipMemcpyHostToDevice, st));
-    // the SpMV of the warm start gathers in A·M coordinates: y0 for precond 0/1, x0 for precond 2
-    const double* gather0 = h_x0 ? (dense ? dx0.p : dy0.p) : nullptr;
+    // the SpMV of the warm start gathers in A·M coordinates: y0 for precond 0/1, x0 for 2 and 3
+    const double* gather0 = h_x0 ? ((dense || block) ? dx0.p : dy0.p) : nullptr;
     hipLaunchKernelGGL(k_init_u, dim3(g.gA), dim3(BLOCK), 0, st, m, S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p,
                        S.rs.p, db.p, gather0, S.A.perm.p, S.u.p, S.bw.p, S.part_u.p, S.part_b.p);
     KERNEL_CHECK();
@@ -557,7 +593,12 @@ void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts&
     KERNEL_CHECK();
     S.vb1.zero(st);
     int nv = g.gT;
-    if (dense) {
+    if (block) {
+        hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
+                           S.AT.val.p, S.u.p, S.vb1.p, S.tt.p, S.part_v.p, 1);
+        launch_block_epi(S, false, g.gB, S.tt.p, S.vb1.p, S.vb0.p, S.zt.p);
+        nv = g.gB;
+    } else if (dense) {
         hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
                            S.AT.val.p, S.u.p, S.vb1.p, S.tt.p, S.part_v.p, 1);
         hipLaunchKernelGGL(k_gemvT_upper, dim3(g.gRT), dim3(BLOCK), 0, st, S.dRi.p, n, S.dense_ld, S.tt.p, S.st.p, 1,
@@ -590,7 +631,7 @@ thread_local GraphCache g_cache;
 
 void launch_any(System& S, const Grids& g, int p, int precond, bool mf) {
     if (mf)
-        launch_iteration_mf(S, g, p);
+        launch_iteration_mf(S, g, p, precond);
     else
         launch_iteration(S, g, p, precond);
 }
@@ -671,6 +712,7 @@ void prepare(System& S, int precond, bool mf) {
     if (!mf) ensure_sell(S);
     refresh_scaling(S, precond);
     if (precond == 2 && !S.dense_valid) dense_factor(S);
+    if (precond == 3 && !S.blk_valid) block_factor(S);
 }
 
 }  // namespace
@@ -707,7 +749,10 @@ int lsqr_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq
     }
     HIP_CHECK(hipEventRecord(e1, S.stream));
     const int64_t n = S.G.n;
-    if (mf)
+    if (o.precond == 3)   // x = M y, block by block, into compact positions
+        hipLaunchKernelGGL(k_block_x, dim3(grid_for(S.nblk)), dim3(BLOCK), 0, S.stream, S.nblk, S.blk_ptr.p,
+                           S.blk_cols.p, mf ? S.blk_full.p : S.blk_cols.p, S.blk_Ri.p, S.y.p, S.vb1.p);
+    else if (mf)
         hipLaunchKernelGGL(k_mf_x, dim3(grid_for(n)), dim3(BLOCK), 0, S.stream, n, S.keep.p, S.y.p, S.csf.p, S.vb1.p);
     else if (o.precond == 2)
         hipLaunchKernelGGL(k_gemv_upper, dim3(g.gR), dim3(BLOCK), 0, S.stream, S.dRi.p, n, S.dense_ld, S.y.p, nullptr,
@@ -810,7 +855,7 @@ void lsqr_profile(System& S, int reps, int op, double* out /* [8] */) {
                 else if (k == 1 && mf)
                     hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, S.stream, S.st.p, S.ATd.sp.p,
                                        S.ATd.ci.p, S.ATd.val.p, S.mfd.p, S.u.p, S.rs.p, S.csf.p, S.vb0.p, S.vb1.p,
-                                       S.zv.p, S.part_v.p);
+                                       S.zv.p, S.part_v.p, 0);
                 else if (k == 1)
                     hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, S.stream, S.st.p, S.G.n, S.AT.nslices,
                                        S.AT.sp.p, S.AT.ci.p, S.AT.val.p, S.u.p, S.vb0.p, S.vb1.p, S.part_v.p, 0);

@@ -127,6 +127,18 @@ struct System {
     DBuf<double> csf;          // column scale in the full space (0 = removed column)
     DBuf<double> zv;           // cs ∘ ṽ in the full space (gathered by the stencil rows)
 
+    // block-Jacobi (precond 3): blocks of compact columns (every kept column in exactly one),
+    // R_b⁻¹ packed upper-triangular by columns, element e = j(j+1)/2 + i of block b at
+    // blk_Ri[e * nblk + b] (structure of arrays: lanes = blocks read contiguously)
+    int64_t nblk = 0;
+    int blk_kmax = 0;
+    bool blk_user = false;          // blocks came from lsq_set_column_blocks
+    DBuf<int64_t> blk_ptr;
+    DBuf<int32_t> blk_cols;         // compact ids
+    DBuf<int32_t> blk_full;         // full ids (stencil operator v-space)
+    DBuf<double> blk_Ri;
+    bool blk_valid = false;
+
     // dense factor (precond 2 / error propagation): R and R⁻¹, npad x npad row-major
     DBuf<double> dR, dRi;
     int64_t dense_ld = 0;
@@ -188,6 +200,11 @@ void scaling_finish_cs(System& S);
 void scaling_fill_values(System& S, int precond);
 bool scaling_stale(const System& S, int precond);
 void csr_spmv(System& S, int trans, const double* dx, double* dy);  // unweighted G / Gᵀ products
+
+// block.hip
+void set_column_blocks(System& S, int64_t nb, const int64_t* ptr, const int32_t* cols);
+void ensure_blocks(System& S);                     // default structure if none was set
+void block_factor(System& S);                      // R_b⁻¹ for the current row scale
 
 // dense.hip
 void dense_factor(System& S);                     // R, R⁻¹ of diag(rs)·G (throws if not SPD)

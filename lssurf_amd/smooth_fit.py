@@ -23,7 +23,7 @@ import numpy as np
 
 from . import containers as pc
 from .calc_sigma_extra import RDE, calc_sigma_extra, calc_sigma_extra_on_grid
-from .constraint_functions import build_reference_epoch_matrix, reference_epoch_keep_cols, \
+from .constraint_functions import build_reference_epoch_matrix, node_column_blocks, reference_epoch_keep_cols, \
     setup_smoothness_constraints
 from .grid_functions import setup_averaging_ops, setup_avg_mask_ops, setup_grids, setup_z0_avg, \
     validate_by_dz_mask
@@ -57,7 +57,7 @@ class FitSystem:
     """The device-resident smooth_fit system: G = [G_data; Gc] (unweighted COO -> device CSR),
     Ip_c as a column map; rows re-weighted / re-selected per outer iteration."""
 
-    def __init__(self, G_data, Gc, keep_cols, n_full, device=0, structured=True):
+    def __init__(self, G_data, Gc, keep_cols, n_full, device=0, structured=True, grids=None):
         self.n_data, self.n_con = int(G_data.N_eq), int(Gc.N_eq)
         self.keep_cols = keep_cols
         self.n_full = int(n_full)
@@ -67,13 +67,19 @@ class FitSystem:
         desc = describe(G_data, Gc) if structured else None
         self.formation = 'stencil' if desc is not None else 'coo'
         if desc is not None:       # rows generated on the device from the grids and stencils
-            grids, interp, coords, stencils, npts = desc
-            self.solver.set_matrix_stencil(m, self.n_full, grids, interp, coords, stencils, npts)
+            gdesc, interp, coords, stencils, npts = desc
+            self.solver.set_matrix_stencil(m, self.n_full, gdesc, interp, coords, stencils, npts)
         else:                      # generic lin_op: host triplets -> device CSR
             r1, c1, v1 = G_data.triplets()
             r2, c2, v2 = Gc.triplets()
             self.solver.set_matrix_coo(m, self.n_full, np.concatenate([r1, r2 + self.n_data]),
                                        np.concatenate([c1, c2]), np.concatenate([v1, v2]))
+        self.has_blocks = False
+        if grids is not None:      # per-node column blocks for the block-Jacobi preconditioner
+            blocks = node_column_blocks(grids, keep_cols)
+            if blocks is not None:
+                self.solver.set_column_blocks_csr(*blocks)
+                self.has_blocks = True
         self.stats = None
 
     def solve(self, row_weight, data_keep, rhs, x0=None, **opts):
@@ -112,12 +118,13 @@ def print_TOC(G_data, Gc):
             print(f'\t{name}: {len(np.unique(rr)) / 1000}K')
 
 
-def _solve_opts(args, n):
+def _solve_opts(args, n, has_blocks=False):
     """LSQR options.  precond 'auto': the exact dense-Cholesky preconditioner (R⁻¹ on the
-    device) when n <= lsq_dense_max, column scaling otherwise (maxit 50 n for those)."""
+    device) when n <= lsq_dense_max, else block-Jacobi per (y, x) node when the system has node
+    blocks, else column scaling (maxit 50 n for the iterative ones)."""
     pc_ = args['lsq_precond']
     if pc_ == 'auto':
-        pc_ = 2 if n <= args['lsq_dense_max'] else 1
+        pc_ = 2 if n <= args['lsq_dense_max'] else (3 if has_blocks else 1)
     maxit = args['lsq_maxit'] or (0 if pc_ == 2 else 50 * n)
     return dict(atol=args['lsq_atol'], btol=args['lsq_btol'], conlim=args['lsq_conlim'], maxit=maxit, precond=pc_)
 
@@ -145,7 +152,7 @@ def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grid
         tic = time()
         m0_last = m0
         x0 = x if (args['lsq_warm_start'] and x is not None) else None
-        x = system.solve(weight, in_TSE, rhs, x0=x0, **_solve_opts(args, system.keep_cols.size))
+        x = system.solve(weight, in_TSE, rhs, x0=x0, **_solve_opts(args, system.keep_cols.size, system.has_blocks))
         if system.stats['istop'] == 7:
             print(f"smooth_fit: LSQR reached its iteration limit ({system.stats['iters']}) before the "
                   f"requested tolerance; raise lsq_maxit or use lsq_precond=2", flush=True)
@@ -325,7 +332,7 @@ def smooth_fit(**kwargs):
     try:
         if args['max_iterations'] > 0:
             tic = time()
-            system = FitSystem(G_data, Gc, keep_cols, Gc.col_N, device=args['device'])
+            system = FitSystem(G_data, Gc, keep_cols, Gc.col_N, device=args['device'], grids=grids)
             timing['device_setup'] = time() - tic
             tic_iteration = time()
             m0, sigma_extra, in_TSE, rs_data = iterate_fit(data, system, rhs, 1. / TCinv_diag, G_data, Gc, in_TSE,

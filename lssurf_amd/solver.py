@@ -93,6 +93,23 @@ class LSQSolver:
         k = None if keep is None else as_c(np.asarray(keep, dtype=bool), np.uint8)
         self._check(self._L.lsq_set_row_mask(self._h, ptr(k)), 'lsq_set_row_mask')
 
+    def set_column_blocks(self, blocks):
+        """Column blocks of the block-Jacobi preconditioner (precond 3): a list of compact-column
+        index arrays (≤ 16 columns each); unlisted columns become singletons.  None clears."""
+        if not blocks:
+            self._check(self._L.lsq_set_column_blocks(self._h, 0, None, None), 'lsq_set_column_blocks')
+            return
+        ptr_ = as_c(np.r_[0, np.cumsum([len(b) for b in blocks])], np.int64)
+        cols = as_c(np.concatenate([np.asarray(b) for b in blocks]), np.int32)
+        self._check(self._L.lsq_set_column_blocks(self._h, len(blocks), ptr(ptr_), ptr(cols)),
+                    'lsq_set_column_blocks')
+
+    def set_column_blocks_csr(self, block_ptr, cols):
+        """Same as set_column_blocks with the blocks given as (block_ptr, cols) arrays."""
+        p_ = as_c(block_ptr, np.int64)
+        c_ = as_c(cols, np.int32)
+        self._check(self._L.lsq_set_column_blocks(self._h, p_.size - 1, ptr(p_), ptr(c_)), 'lsq_set_column_blocks')
+
     def shape(self):
         m, n, z = (ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64())
         self._check(self._L.lsq_shape(self._h, ctypes.byref(m), ctypes.byref(n), ctypes.byref(z)), 'lsq_shape')

@@ -301,3 +301,78 @@ def test_stencil_operator_mask_reweight_warm_start(gpu_available):
     assert np.linalg.norm(x1 - x0) / np.linalg.norm(x0) <= 1e-8
     assert np.linalg.norm(x2 - x0) / np.linalg.norm(x0) <= 1e-8
     assert it_warm < it_cold
+
+
+def _t64_blocks():
+    from lssurf_amd import synthetic
+    D, kw = synthetic.points('t64')
+    S = LS.smooth_fit(data=D, return_fit_objects=True, VERBOSE=False, **kw)
+    keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch'])
+    fs = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, grids=S['grids'])
+    E_all = 1 / (1. / np.concatenate((S['Ed'], S['Ec'])))
+    w = 1. / np.sqrt(E_all ** 2)
+    rhs = np.zeros(w.size)
+    rhs[:S['data'].size] = S['data'].z
+    return S, fs, w, rhs
+
+
+@pytest.mark.parametrize('name', SYSTEMS)
+def test_block_jacobi_matches_exact_solution(gpu_available, name):
+    g = golden(f'sys_{name}.npz')
+    kw = golden_kwargs(g)
+    S = LS.smooth_fit(data=golden_points(g), return_fit_objects=True, **kw)
+    keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch'])
+    fs = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, grids=S['grids'])
+    E_all = 1 / (1. / np.concatenate((S['Ed'], S['Ec'])))
+    w = 1. / np.sqrt(E_all ** 2)
+    rhs = np.zeros(w.size)
+    rhs[:S['data'].size] = S['data'].z
+    try:
+        assert fs.has_blocks
+        x = fs.solve(w, np.ones(fs.n_data, bool), rhs, atol=1e-12, btol=1e-12, conlim=1e12, precond=3)
+        st = fs.stats
+    finally:
+        fs.close()
+    xs = g['x']
+    assert st['istop'] in (1, 2), st
+    assert np.linalg.norm(x - xs) / np.linalg.norm(xs) <= REL
+    assert np.max(np.abs(x - xs)) <= ABS
+
+
+def test_block_jacobi_both_operators_and_fewer_iterations(gpu_available):
+    S, fs, w, rhs = _t64_blocks()
+    keep = np.ones(fs.n_data, bool)
+    tol = dict(atol=1e-12, btol=1e-12, conlim=1e12)
+    try:
+        x1 = fs.solve(w, keep, rhs, precond=1, **tol)
+        it1 = fs.stats['iters']
+        xb0 = fs.solve(w, keep, rhs, precond=3, op=0, **tol)
+        itb0 = fs.stats['iters']
+        xb1 = fs.solve(w, keep, rhs, precond=3, op=1, **tol)
+        itb1 = fs.stats['iters']
+        xw = fs.solve(w, keep, rhs, x0=xb0, precond=3, **tol)
+        itw = fs.stats['iters']
+    finally:
+        fs.close()
+    for x in (xb0, xb1, xw):
+        assert np.linalg.norm(x - x1) / np.linalg.norm(x1) <= 1e-8
+    assert abs(itb0 - itb1) <= max(3, 0.02 * itb0)
+    assert itb0 < it1, (itb0, it1)
+    assert itw < itb0
+
+
+def test_column_blocks_validation(gpu_available):
+    S, fs, w, rhs = _t64_blocks()
+    try:
+        with pytest.raises(Exception):
+            fs.solver.set_column_blocks([np.arange(17)])          # too long
+        with pytest.raises(Exception):
+            fs.solver.set_column_blocks([[0, 1], [1, 2]])         # column in two blocks
+        with pytest.raises(Exception):
+            fs.solver.set_column_blocks([[0, 10 ** 9]])          # out of range
+        fs.solver.set_column_blocks(None)                        # all singletons = Jacobi scaling
+        x = fs.solve(w, np.ones(fs.n_data, bool), rhs, precond=3, atol=1e-12, btol=1e-12, conlim=1e12)
+        x1 = fs.solve(w, np.ones(fs.n_data, bool), rhs, precond=1, atol=1e-12, btol=1e-12, conlim=1e12)
+    finally:
+        fs.close()
+    assert np.linalg.norm(x - x1) / np.linalg.norm(x1) <= 1e-8
