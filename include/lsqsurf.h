@@ -173,6 +173,16 @@ int lsq_dist_set_layout(lsq_handle* h, const int32_t* col_local, int64_t n_local
                         int32_t n_peers, const int32_t* peers, const int64_t* send_cnt,
                         const int32_t* send_idx, const int64_t* recv_cnt);
 
+/* Structured-operator ranks (systems formed by lsq_set_matrix_stencil): each rank forms its
+ * window of node rows — owned rows ± halo rows, as sub-grids with their own column numbering —
+ * and installs the halo: own_ranges = n_ranges [start, end) pairs of owned local full columns;
+ * per peer, send_idx lists owned local columns that peer holds as ghosts and recv_idx the local
+ * ghost columns that peer owns (both in ascending GLOBAL column order).  lsq_solve then returns
+ * every local compact column in x_inout (length = the local compact width; ghosts come out 0). */
+int lsq_dist_set_halo(lsq_handle* h, int32_t n_ranges, const int64_t* own_ranges, int32_t n_peers,
+                      const int32_t* peers, const int64_t* send_cnt, const int32_t* send_idx,
+                      const int64_t* recv_cnt, const int32_t* recv_idx);
+
 /* Virtual ranks: the same distributed solve with every rank of the partition in THIS process
  * on one device (exchanges become device copies).  Configure each rank's handle exactly as a
  * real rank (lsq_set_col_map, lsq_set_matrix_*, lsq_dist_referenced_cols,

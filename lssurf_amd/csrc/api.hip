@@ -381,6 +381,72 @@ int lsq_dist_set_layout(lsq_handle* h, const int32_t* col_local, int64_t n_local
     });
 }
 
+int lsq_dist_set_halo(lsq_handle* h, int32_t n_ranges, const int64_t* own_ranges, int32_t n_peers,
+                      const int32_t* peers, const int64_t* send_cnt, const int32_t* send_idx,
+                      const int64_t* recv_cnt, const int32_t* recv_idx) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.comm && !S.virt)
+            return fail(S, "lsq_dist_set_halo: handle has no communicator (use lsq_create_dist / lsq_vgroup)");
+        if (!S.G.rp.p || S.dist) return fail(S, "lsq_dist_set_halo: needs a formed matrix, once");
+        if (!S.mf) return fail(S, "lsq_dist_set_halo: needs a structured system (lsq_set_matrix_stencil)");
+        if (n_ranges < 0 || (n_ranges && !own_ranges) || n_peers < 0) return fail(S, "lsq_dist_set_halo: bad args");
+        const int64_t nf = S.n_full;
+        std::vector<uint8_t> own(nf, 0);
+        for (int i = 0; i < n_ranges; ++i) {
+            const int64_t a = own_ranges[2 * i], b = own_ranges[2 * i + 1];
+            if (a < 0 || b > nf || a > b) return fail(S, "lsq_dist_set_halo: owned range outside the local columns");
+            std::fill(own.begin() + a, own.begin() + b, 1);
+        }
+        S.peers.assign(peers, peers + n_peers);
+        S.send_cnt.assign(send_cnt, send_cnt + n_peers);
+        S.recv_cnt.assign(recv_cnt, recv_cnt + n_peers);
+        S.send_off.assign(n_peers, 0);
+        S.recv_off.assign(n_peers, 0);
+        int64_t ts = 0, tr = 0;
+        for (int k = 0; k < n_peers; ++k) {
+            if (peers[k] < 0 || peers[k] >= S.nranks || peers[k] == S.rank)
+                return fail(S, "lsq_dist_set_halo: bad peer rank");
+            S.send_off[k] = ts;
+            S.recv_off[k] = tr;
+            ts += send_cnt[k];
+            tr += recv_cnt[k];
+        }
+        for (int64_t k = 0; k < ts; ++k)
+            if (send_idx[k] < 0 || send_idx[k] >= nf || !own[send_idx[k]])
+                return fail(S, "lsq_dist_set_halo: send index not an owned local column");
+        for (int64_t k = 0; k < tr; ++k)
+            if (recv_idx[k] < 0 || recv_idx[k] >= nf || own[recv_idx[k]])
+                return fail(S, "lsq_dist_set_halo: receive index not a ghost local column");
+        // live = owned and kept (Ip_c)
+        std::vector<int32_t> keep(S.G.n);
+        S.keep.download(keep.data(), S.G.n, S.stream);
+        HIP_CHECK(hipStreamSynchronize(S.stream));
+        std::vector<uint8_t> live(nf, 0);
+        for (int32_t f : keep) live[f] = own[f];
+        lsq::graph_cache_drop(&S);
+        S.live.alloc(std::max<int64_t>(nf, 1));
+        S.live.upload(live.data(), nf, S.stream);
+        S.send_idx.alloc(std::max<int64_t>(ts, 1));
+        S.send_idx.upload(send_idx, ts, S.stream);
+        S.send_idx.n = ts;
+        S.recv_idx.alloc(std::max<int64_t>(tr, 1));
+        S.recv_idx.upload(recv_idx, tr, S.stream);
+        S.recv_idx.n = tr;
+        const int64_t nb = std::max<int64_t>(std::max(ts, tr), 1);
+        S.sbuf.alloc(nb);
+        S.rbuf.alloc(nb);
+        S.gsum.alloc(8);
+        S.gsum.zero(S.stream);
+        HIP_CHECK(hipStreamSynchronize(S.stream));
+        S.n_own = S.G.n;
+        S.dist = true;
+        S.dist_mf = true;
+        S.cs_mode = -1;
+        S.iter_ready = false;
+        return 0;
+    });
+}
+
 int lsq_sigma_x(lsq_handle* h, double* E) {
     return guarded(h, [&](lsq::System& S) {
         if (!S.G.rp.p) return fail(S, "lsq_sigma_x: no matrix");

@@ -332,7 +332,7 @@ void form_from_stencils(System& S, int64_t m, int64_t n_full, int32_t n_grids, c
     if (herr) throw std::invalid_argument("lsq_set_matrix_stencil: " + std::to_string(herr) +
                                           " nonzero entries fall outside [0, n_full)");
     S.n_sorted_rows = npts;   // data rows: point order is random in space
-    S.mf = !S.dist && !S.comm && !S.virt && describe_stencil_operator(S.mfh, m, n_full, n_grids, grids, npts, n_stencil, st);
+    S.mf = !S.dist && describe_stencil_operator(S.mfh, m, n_full, n_grids, grids, npts, n_stencil, st);
     finish_formation(S);
 }
 

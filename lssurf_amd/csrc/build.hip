@@ -651,7 +651,7 @@ void scaling_finish_cs(System& S) {
     KERNEL_CHECK();
 }
 
-void scaling_fill_values(System& S, int precond) {
+void scaling_fill_values(System& S, int precond, bool set_csf) {
     hipStream_t st = S.stream;
     const int64_t m = S.G.m, n = S.G.n;
     if (S.sell_built) {
@@ -670,9 +670,11 @@ void scaling_fill_values(System& S, int precond) {
         hipLaunchKernelGGL(k_sell_vals, dim3(grid_for(S.ATd.rows)), dim3(BLOCK), 0, st, S.ATd.rows, S.GdT.rp.p,
                            S.GdT.ci.p, S.GdT.val.p, S.rs.p, nullptr, 1, S.ATd.perm.p, S.ATd.sp.p, S.ATd.val.p);
         KERNEL_CHECK();
-        S.csf.zero(st);
-        hipLaunchKernelGGL(k_scatter_cs, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, S.keep.p, S.cs.p, S.csf.p);
-        KERNEL_CHECK();
+        if (set_csf) {   // distributed ranks assemble csf themselves (column norms span ranks)
+            S.csf.zero(st);
+            hipLaunchKernelGGL(k_scatter_cs, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, S.keep.p, S.cs.p, S.csf.p);
+            KERNEL_CHECK();
+        }
         // parts whose rows share one row scale skip the per-row scale loads in the iteration
         const int np = S.mfh.n_parts;
         DBuf<double> mm(2 * np);

@@ -822,7 +822,7 @@ void lsqr_profile(System& S, int reps, int op, double* out /* [8] */) {
     lsq_opts o;
     lsq_default_opts(&o);
     o.op = op;
-    const bool mf = use_mf(S, o);
+    const bool mf = S.dist ? S.dist_mf : use_mf(S, o);
     if (!S.dist) prepare(S, 1, mf);   // a distributed rank keeps the scaling its group filled
     ensure_workspace(S);
     const Grids g = grids_for(S);

@@ -159,6 +159,12 @@ struct System {
     DBuf<int32_t> send_idx;         // concatenated by peer: owned local column indices
     DBuf<double> sbuf, rbuf;        // packed forward values / received reverse partials
     DBuf<double> gsum;              // [0] Σu², [1] Σw², [2] Σṽ², [3] Σb² (all-reduced)
+    // structured-operator ranks (lsq_dist_set_halo): the local system is the rank's window of
+    // node rows (owned rows ± halo rows) on sub-grids; v-space = local full columns; halos move
+    // the listed local full ids (send_idx: owned, recv_idx: ghosts), live = owned ∧ kept
+    bool dist_mf = false;
+    DBuf<int32_t> recv_idx;
+    DBuf<uint8_t> live;
 
     // LSQR workspace
     DBuf<double> u, vb0, vb1, w, y, bw, zt, tt;
@@ -197,7 +203,7 @@ void ensure_sell(System& S);                    // assembled A / AT (lazy when S
 void refresh_scaling(System& S, int precond);   // rs/cs -> SELL values (single GPU)
 void scaling_rows_colnorm(System& S, int precond, bool raw);
 void scaling_finish_cs(System& S);
-void scaling_fill_values(System& S, int precond);
+void scaling_fill_values(System& S, int precond, bool set_csf = true);
 bool scaling_stale(const System& S, int precond);
 void csr_spmv(System& S, int trans, const double* dx, double* dy);  // unweighted G / Gᵀ products
 

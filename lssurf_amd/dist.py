@@ -80,6 +80,141 @@ def rank_problem(G_data, Gc, partition, rank):
                 npts=int(pts_own.size), rows=np.concatenate(rows), m=int(row0))
 
 
+def _describe_order(G_data, Gc):
+    desc = assemble.describe(G_data, Gc)
+    if desc is None:
+        raise NotImplementedError('distributed solve needs a structured (stencil + interp) system')
+    order, seen = [], set()
+    for p in list(G_data.parts) + list(Gc.parts):
+        if id(p['grid']) not in seen:
+            seen.add(id(p['grid']))
+            order.append(p['grid'])
+    return desc, order
+
+
+def window_meta(grid_objs, partition, rank, halo):
+    """Per grid: (wa, wb, a, b) = window rows [wa, wb) = owned rows [a, b) ± halo rows, and the
+    local column offset of the grid's window (grids in global column order)."""
+    meta, col0 = [], 0
+    for g in grid_objs:
+        a, b = partition.rows_of(g, rank)
+        if a >= b:
+            raise ValueError(f'rank {rank} owns no node rows of a grid: too many ranks for the grid')
+        ny = int(g.shape[0])
+        wa, wb = max(0, a - halo), min(ny, b + halo)
+        stride = int(g.stride[0])
+        meta.append(dict(wa=wa, wb=wb, a=a, b=b, stride=stride, col0=col0, gcol0=int(g.col_0)))
+        col0 += (wb - wa) * stride
+    return meta, col0
+
+
+def window_problem(G_data, Gc, partition, rank, keep_cols):
+    """The rank's window of the structured system: sub-grids of its owned node rows ± halo rows
+    (own column numbering), the stencil parts clipped to its owned centre rows, its points, and
+    the maps to the global system.  Every rank computes every window (no communication)."""
+    from ._native import GridDesc
+    (grid_descs, interp, (py, px, pt), stencils, npts), order = _describe_order(G_data, Gc)
+    halo = max([1] + [abs(int(s.off[t][0])) for s in stencils for t in range(s.ntpl)])
+    meta, nloc = window_meta(order, partition, rank, halo)
+    grids = []
+    for gd, gm in zip(grid_descs, meta):
+        d = GridDesc.from_buffer_copy(gd)
+        d.shape[0] = gm['wb'] - gm['wa']
+        d.b0[0] = gd.b0[0] + gm['wa'] * gd.delta[0]
+        d.col0 = gm['col0']
+        grids.append(d)
+    pts_own = np.flatnonzero(partition.owner(py) == rank)
+    rows = [pts_own]
+    local = []
+    row0 = pts_own.size
+    for s, part in zip(stencils, Gc.parts):
+        gm = meta[s.grid]
+        lo_y, hi_y = max(int(s.lo[0]), gm['a']), min(int(s.hi[0]), gm['b'])
+        if lo_y >= hi_y:
+            continue
+        nd = int(order[s.grid].N_dims)
+        inner = int(np.prod([int(s.hi[d]) - int(s.lo[d]) for d in range(1, nd)]))
+        t = type(s).from_buffer_copy(s)
+        t.lo[0], t.hi[0] = lo_y - gm['wa'], hi_y - gm['wa']
+        t.n_eq = (hi_y - lo_y) * inner
+        t.row0 = row0
+        first = npts + int(part['row0']) + (lo_y - int(s.lo[0])) * inner
+        rows.append(first + np.arange(t.n_eq))
+        row0 += t.n_eq
+        local.append(t)
+    coords = (py[pts_own].copy(), px[pts_own].copy(), None if pt is None else pt[pts_own].copy())
+    l2g = np.concatenate([gm['gcol0'] + gm['wa'] * gm['stride'] + np.arange((gm['wb'] - gm['wa']) * gm['stride'])
+                          for gm in meta])
+    keep_cols = np.asarray(keep_cols)
+    pos = np.minimum(np.searchsorted(keep_cols, l2g), keep_cols.size - 1)
+    keep_local = np.flatnonzero(keep_cols[pos] == l2g)
+    own_ranges = [(gm['col0'] + (gm['a'] - gm['wa']) * gm['stride'], gm['col0'] + (gm['b'] - gm['wa']) * gm['stride'])
+                  for gm in meta]
+    return dict(grids=grids, grid_objs=order, interp=interp, coords=coords, stencils=local, npts=int(pts_own.size),
+                rows=np.concatenate(rows), m=int(row0), n_full=int(nloc), keep=keep_local, l2g=l2g,
+                keep_global=pos[keep_local], own_ranges=own_ranges, meta=meta, halo=halo)
+
+
+def window_halo(grid_objs, partition, rank, halo):
+    """Halo lists of `rank` (local full ids, ascending global order): per peer, the owned
+    columns the peer holds as ghosts (send) and the ghost columns the peer owns (recv)."""
+    nr = partition.nranks
+    metas = [window_meta(grid_objs, partition, r, halo)[0] for r in range(nr)]
+    mine = metas[rank]
+    peers, send, recv = [], [], []
+    for p in range(nr):
+        if p == rank:
+            continue
+        s_ids, r_ids = [], []
+        for gm, gp in zip(mine, metas[p]):
+            lo, hi = max(gm['a'], gp['wa']), min(gm['b'], gp['wb'])        # my owned rows in p's window
+            if lo < hi:
+                s_ids.append(gm['col0'] + (lo - gm['wa']) * gm['stride'] + np.arange((hi - lo) * gm['stride']))
+            lo, hi = max(gm['wa'], gp['a']), min(gm['wb'], gp['b'])        # p's owned rows in my window
+            if lo < hi:
+                r_ids.append(gm['col0'] + (lo - gm['wa']) * gm['stride'] + np.arange((hi - lo) * gm['stride']))
+        if s_ids or r_ids:
+            peers.append(p)
+            send.append(np.concatenate(s_ids) if s_ids else np.zeros(0, np.int64))
+            recv.append(np.concatenate(r_ids) if r_ids else np.zeros(0, np.int64))
+    cat = lambda xs: np.concatenate(xs).astype(np.int32) if xs else np.zeros(0, np.int32)
+    return (np.array(peers, np.int32), np.array([x.size for x in send], np.int64), cat(send),
+            np.array([x.size for x in recv], np.int64), cat(recv))
+
+
+def _form_window(L, h, prob):
+    from ._native import GridDesc, StencilDesc
+    s = _HandleView(L, h)
+    keep = as_c(prob['keep'], np.int64)
+    s.check(L.lsq_set_col_map(h, prob['n_full'], ptr(keep), keep.size), 'lsq_set_col_map')
+    ga = (GridDesc * len(prob['grids']))(*prob['grids'])
+    sa = (StencilDesc * max(len(prob['stencils']), 1))(*prob['stencils'])
+    ig = as_c(np.asarray(prob['interp'], np.int32), np.int32)
+    py, px, pt = prob['coords']
+    s.check(L.lsq_set_matrix_stencil(h, prob['m'], prob['n_full'], len(prob['grids']),
+                                     ctypes.cast(ga, ctypes.c_void_p), len(prob['interp']), ptr(ig), prob['npts'],
+                                     ptr(py), ptr(px), ptr(pt), len(prob['stencils']), ctypes.cast(sa, ctypes.c_void_p),
+                                     None), 'lsq_set_matrix_stencil')
+
+
+def _install_halo(L, h, prob, halo):
+    peers, send_cnt, send_idx, recv_cnt, recv_idx = halo
+    rng = as_c(np.asarray(prob['own_ranges'], np.int64).ravel(), np.int64)
+    _HandleView(L, h).check(
+        L.lsq_dist_set_halo(h, len(prob['own_ranges']), ptr(rng), peers.size, ptr(peers), ptr(send_cnt),
+                            ptr(send_idx), ptr(recv_cnt), ptr(recv_idx)), 'lsq_dist_set_halo')
+
+
+def window_owned_solution(prob, x_local, x_out):
+    """Scatter the owned columns of a rank's local compact solution into the global compact x."""
+    full = prob['keep']
+    own = np.zeros(prob['n_full'], bool)
+    for a, b in prob['own_ranges']:
+        own[a:b] = True
+    sel = own[full]
+    x_out[prob['keep_global'][sel]] = x_local[sel]
+
+
 def column_owner(keep_cols, grid_objs, partition):
     """Owner rank of every compact column (global full column -> its grid node row -> y)."""
     full = np.asarray(keep_cols)
@@ -191,12 +326,13 @@ class DistFitSystem(_Base):
     """One rank of a multi-GPU solve (RCCL).  `pg` is a torch.distributed process group used only
     for set-up (RCCL id broadcast, ghost lists); the solve itself never touches torch."""
 
-    def __init__(self, G_data, Gc, keep_cols, n_full, rank, nranks, device, pg=None):
+    def __init__(self, G_data, Gc, keep_cols, n_full, rank, nranks, device, pg=None, structured=True):
         if nranks > 1:
             import torch.distributed as tdist
         self.L = load()
         self._setup_common(G_data, Gc, keep_cols, n_full, nranks)
         self.rank, self.nranks = rank, nranks
+        self.structured = structured
         uid = np.zeros(128, np.uint8)
         if rank == 0 and self.L.lsq_dist_unique_id(ptr(uid)) != 0:
             raise NativeError('lsq_dist_unique_id failed')
@@ -207,18 +343,33 @@ class DistFitSystem(_Base):
         self.h = _quiet_stdout(lambda: self.L.lsq_create_dist(int(device), int(rank), int(nranks), ptr(uid)))
         if not self.h:
             raise NativeError('lsq_create_dist failed (RCCL communicator)')
-        self.prob = rank_problem(G_data, Gc, self.partition, rank)
-        flags = _form_rank(self.L, self.h, self.prob, keep_cols, n_full)
-        owner = column_owner(keep_cols, self.prob['grid_objs'], self.partition)
-        self.layout = local_layout(flags, owner, rank)
-        gathered = [self.layout[3]]
-        if nranks > 1:
-            gathered = [None] * nranks
-            tdist.all_gather_object(gathered, self.layout[3], group=pg)
-        self.plan = exchange_plan(rank, self.layout[0], gathered)
-        _install_layout(self.L, self.h, self.layout, self.plan)
-        self.owned_cols = self.layout[4]
+        if structured:   # window of node rows on sub-grids, structured stencil operator
+            self.prob = window_problem(G_data, Gc, self.partition, rank, keep_cols)
+            _form_window(self.L, self.h, self.prob)
+            _install_halo(self.L, self.h, self.prob,
+                          window_halo(self.prob['grid_objs'], self.partition, rank, self.prob['halo']))
+            self.n_x = self.prob['keep'].size
+        else:            # owned rows, relabelled compact columns, assembled SELL operator
+            self.prob = rank_problem(G_data, Gc, self.partition, rank)
+            flags = _form_rank(self.L, self.h, self.prob, keep_cols, n_full)
+            owner = column_owner(keep_cols, self.prob['grid_objs'], self.partition)
+            self.layout = local_layout(flags, owner, rank)
+            gathered = [self.layout[3]]
+            if nranks > 1:
+                gathered = [None] * nranks
+                tdist.all_gather_object(gathered, self.layout[3], group=pg)
+            self.plan = exchange_plan(rank, self.layout[0], gathered)
+            _install_layout(self.L, self.h, self.layout, self.plan)
+            self.owned_cols = self.layout[4]
+            self.n_x = self.layout[2]
         self.stats = None
+
+    def scatter_owned(self, x_local, x_out):
+        """Owned columns of this rank's solution into the global compact vector x_out."""
+        if self.structured:
+            window_owned_solution(self.prob, x_local, x_out)
+        else:
+            x_out[self.owned_cols] = x_local
 
     def _b(self, row_weight, rhs):
         """None keeps the weights / local rhs of the previous call (no host slicing)."""
@@ -234,13 +385,13 @@ class DistFitSystem(_Base):
 
     def solve(self, row_weight, rhs, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1):
         b = self._b(row_weight, rhs)
-        x = np.zeros(self.layout[2])
+        x = np.zeros(self.n_x)
         o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond))
         st = LsqStats()
         _HandleView(self.L, self.h).check(self.L.lsq_solve(self.h, ptr(b), ptr(x), ctypes.byref(o), ctypes.byref(st)),
                                           'lsq_solve')
         self.stats = st.as_dict()
-        return x   # owned compact columns self.owned_cols
+        return x   # this rank's columns: scatter_owned() places them in the global vector
 
     def iterate(self, row_weight, rhs, iters, precond=1):
         b = self._b(row_weight, rhs)
@@ -265,25 +416,37 @@ class VirtualDistFitSystem(_Base):
     """All ranks of the partition in this process on one GPU (liblsqsurf virtual group):
     identical kernels, plans and exchange order as the RCCL path."""
 
-    def __init__(self, G_data, Gc, keep_cols, n_full, nranks, device=0):
+    def __init__(self, G_data, Gc, keep_cols, n_full, nranks, device=0, structured=True):
         self.L = load()
         self._setup_common(G_data, Gc, keep_cols, n_full, nranks)
         self.nranks = nranks
+        self.structured = structured
         self.g = self.L.lsq_vgroup_create(int(device), int(nranks))
         if not self.g:
             raise NativeError('lsq_vgroup_create failed')
-        self.probs, self.layouts, flags_all = [], [], []
-        for r in range(nranks):
-            h = self.L.lsq_vgroup_rank(self.g, r)
-            prob = rank_problem(G_data, Gc, self.partition, r)
-            flags_all.append(_form_rank(self.L, h, prob, keep_cols, n_full))
-            self.probs.append(prob)
-        owner = column_owner(keep_cols, self.probs[0]['grid_objs'], self.partition)
-        self.layouts = [local_layout(flags_all[r], owner, r) for r in range(nranks)]
-        ghosts_of = [lay[3] for lay in self.layouts]
-        for r in range(nranks):
-            _install_layout(self.L, self.L.lsq_vgroup_rank(self.g, r), self.layouts[r],
-                            exchange_plan(r, self.layouts[r][0], ghosts_of))
+        self.probs = []
+        if structured:
+            for r in range(nranks):
+                h = self.L.lsq_vgroup_rank(self.g, r)
+                prob = window_problem(G_data, Gc, self.partition, r, keep_cols)
+                _form_window(self.L, h, prob)
+                _install_halo(self.L, h, prob, window_halo(prob['grid_objs'], self.partition, r, prob['halo']))
+                self.probs.append(prob)
+            self.nx = [p['keep'].size for p in self.probs]
+        else:
+            flags_all = []
+            for r in range(nranks):
+                h = self.L.lsq_vgroup_rank(self.g, r)
+                prob = rank_problem(G_data, Gc, self.partition, r)
+                flags_all.append(_form_rank(self.L, h, prob, keep_cols, n_full))
+                self.probs.append(prob)
+            owner = column_owner(keep_cols, self.probs[0]['grid_objs'], self.partition)
+            self.layouts = [local_layout(flags_all[r], owner, r) for r in range(nranks)]
+            ghosts_of = [lay[3] for lay in self.layouts]
+            for r in range(nranks):
+                _install_layout(self.L, self.L.lsq_vgroup_rank(self.g, r), self.layouts[r],
+                                exchange_plan(r, self.layouts[r][0], ghosts_of))
+            self.nx = [lay[2] for lay in self.layouts]
         self.stats = None
 
     def _check(self, rc, what):
@@ -302,7 +465,7 @@ class VirtualDistFitSystem(_Base):
 
     def solve(self, row_weight, rhs, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1):
         bs = self._bs(row_weight, rhs)
-        xs = [np.zeros(lay[2]) for lay in self.layouts]
+        xs = [np.zeros(k) for k in self.nx]
         bp = (ctypes.c_void_p * self.nranks)(*[b.ctypes.data for b in bs])
         xp = (ctypes.c_void_p * self.nranks)(*[x.ctypes.data for x in xs])
         o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond))
@@ -310,8 +473,11 @@ class VirtualDistFitSystem(_Base):
         self._check(self.L.lsq_vgroup_solve(self.g, bp, xp, ctypes.byref(o), ctypes.byref(st)), 'lsq_vgroup_solve')
         self.stats = st.as_dict()
         x = np.zeros(self.keep_cols.size)
-        for lay, xr in zip(self.layouts, xs):
-            x[lay[4]] = xr
+        for r, xr in enumerate(xs):
+            if self.structured:
+                window_owned_solution(self.probs[r], xr, x)
+            else:
+                x[self.layouts[r][4]] = xr
         return x   # compact columns (same space as LSQSolver.solve)
 
     def iterate(self, row_weight, rhs, iters, precond=1):

@@ -128,3 +128,30 @@ def test_gloo_world2_plan_exchange():
     for p in procs:
         p.join(60)
     assert res == {0: 'ok', 1: 'ok'}, res
+
+
+@pytest.mark.parametrize('nranks', [2, 3, 4])
+def test_windows_partition_rows_and_columns(nranks):
+    """Structured-operator ranks: every row in exactly one window, owned columns tile the
+    compact space, halo lists mirror each other (same global columns, same order)."""
+    S, keep = _system()
+    part = dist.SlabPartition(S['grids']['dz'], nranks)
+    m = S['G_data'].N_eq + S['Gc'].N_eq
+    probs = [dist.window_problem(S['G_data'], S['Gc'], part, r, keep) for r in range(nranks)]
+    np.testing.assert_array_equal(np.sort(np.concatenate([p['rows'] for p in probs])), np.arange(m))
+    x = np.zeros(keep.size)
+    for p in probs:
+        dist.window_owned_solution(p, np.ones(p['keep'].size), x)
+    assert np.all(x == 1.0)
+    assert sum(int(np.sum([b - a for a, b in p['own_ranges']])) for p in probs) == S['Gc'].col_N
+    halos = [dist.window_halo(p['grid_objs'], part, r, p['halo']) for r, p in enumerate(probs)]
+    for r, (peers, sc, si, rc, ri) in enumerate(halos):
+        so, ro = np.r_[0, np.cumsum(sc)], np.r_[0, np.cumsum(rc)]
+        for k, q in enumerate(peers):
+            pq = halos[q]
+            kk = list(pq[0]).index(r)
+            qso = np.r_[0, np.cumsum(pq[1])]
+            mine_sent = probs[r]['l2g'][si[so[k]:so[k + 1]]]
+            theirs_recv = probs[q]['l2g'][pq[4][np.r_[0, np.cumsum(pq[3])][kk]:np.r_[0, np.cumsum(pq[3])][kk + 1]]]
+            np.testing.assert_array_equal(mine_sent, theirs_recv)
+            assert np.all(np.diff(mine_sent) > 0)

@@ -45,12 +45,13 @@ def _single(S, keep, w, rhs):
     return x, st
 
 
+@pytest.mark.parametrize('structured', [True, False])
 @pytest.mark.parametrize('nranks', [2, 3, 4])
-def test_virtual_ranks_match_single_gpu(gpu_available, nranks):
+def test_virtual_ranks_match_single_gpu(gpu_available, nranks, structured):
     S, kw = _t64()
     keep, w, rhs = _problem(S, kw)
     x1, st1 = _single(S, keep, w, rhs)
-    vd = dist.VirtualDistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, nranks)
+    vd = dist.VirtualDistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, nranks, structured=structured)
     try:
         xd = vd.solve(w, rhs, **TOL)
         std = vd.stats
@@ -61,12 +62,13 @@ def test_virtual_ranks_match_single_gpu(gpu_available, nranks):
     assert np.linalg.norm(xd - x1) / np.linalg.norm(x1) <= 1e-8
 
 
-def test_virtual_ranks_golden_exact_solution(gpu_available):
+@pytest.mark.parametrize('structured', [True, False])
+def test_virtual_ranks_golden_exact_solution(gpu_available, structured):
     g = golden('sys_sf3d.npz')
     kw = golden_kwargs(g)
     S = LS.smooth_fit(data=golden_points(g), return_fit_objects=True, **kw)
     keep, w, rhs = _problem(S, kw)
-    vd = dist.VirtualDistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, 2)
+    vd = dist.VirtualDistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, 2, structured=structured)
     try:
         x = vd.solve(w, rhs, atol=1e-12, btol=1e-12, conlim=1e12, maxit=200000, precond=1)
     finally:
@@ -76,11 +78,12 @@ def test_virtual_ranks_golden_exact_solution(gpu_available):
     assert np.max(np.abs(x - xs)) <= 1e-4
 
 
-def test_virtual_ranks_reweight_and_iterate(gpu_available):
+@pytest.mark.parametrize('structured', [True, False])
+def test_virtual_ranks_reweight_and_iterate(gpu_available, structured):
     """Row weights change between solves (the editing loop); fixed-iteration runs work."""
     S, kw = _t64()
     keep, w, rhs = _problem(S, kw)
-    vd = dist.VirtualDistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, 2)
+    vd = dist.VirtualDistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, 2, structured=structured)
     try:
         st = vd.iterate(w, rhs, 40)
         assert st['iters'] == 40
@@ -93,7 +96,8 @@ def test_virtual_ranks_reweight_and_iterate(gpu_available):
     assert np.linalg.norm(xd - x1) / np.linalg.norm(x1) <= 1e-8
 
 
-def test_rccl_one_rank(gpu_available):
+@pytest.mark.parametrize('structured', [True, False])
+def test_rccl_one_rank(gpu_available, structured):
     """DistFitSystem over a one-rank RCCL communicator (the N=1 case of bench --gpus N)."""
     import torch.distributed as tdist
     S, kw = _t64()
@@ -104,7 +108,7 @@ def test_rccl_one_rank(gpu_available):
         port = s.getsockname()[1]
     tdist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=0, world_size=1)
     try:
-        ds = dist.DistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, 0, 1, device=0)
+        ds = dist.DistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, 0, 1, device=0, structured=structured)
         try:
             xo = ds.solve(w, rhs, **TOL)
             std = ds.stats
@@ -113,6 +117,6 @@ def test_rccl_one_rank(gpu_available):
     finally:
         tdist.destroy_process_group()
     x = np.zeros(keep.size)
-    x[ds.owned_cols] = xo
+    ds.scatter_owned(xo, x)
     assert std['istop'] in (1, 2)
     assert np.linalg.norm(x - x1) / np.linalg.norm(x1) <= 1e-8
