@@ -292,10 +292,8 @@ int lsq_sell_info(lsq_handle* h, int64_t* out8) {
         out8[0] = S.G.m;
         out8[1] = S.G.n;
         out8[2] = S.G.nnz;
-        const lsq::Sell& a = S.mf ? S.Ad : S.A;
-        const lsq::Sell& t = S.mf ? S.ATd : S.AT;
-        out8[3] = a.nent;
-        out8[4] = t.nent;
+        out8[3] = S.mf ? S.Ad.nent : S.A.nent;
+        out8[4] = S.mf ? S.ATd.nnz : S.AT.nent;
         out8[5] = (int64_t)(S.G.rp.bytes() + S.G.ci.bytes() + S.G.val.bytes() + S.GT.rp.bytes() + S.GT.ci.bytes() +
                             S.GT.val.bytes() + S.A.ci.bytes() + S.A.val.bytes() + S.AT.ci.bytes() + S.AT.val.bytes() +
                             S.Ad.ci.bytes() + S.Ad.val.bytes() + S.ATd.ci.bytes() + S.ATd.val.bytes() +

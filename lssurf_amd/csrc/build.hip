@@ -567,6 +567,56 @@ void ensure_sell(System& S) {
 
 namespace {
 
+__global__ __launch_bounds__(BLOCK) void k_c32_count(int64_t rows, const int32_t* __restrict__ perm,
+                                                     const int64_t* __restrict__ srp, int64_t* __restrict__ cnt) {
+    for (int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BLOCK) {
+        const int32_t q = perm[r];
+        cnt[r] = q >= 0 ? srp[q + 1] - srp[q] : 0;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_c32_fill(int64_t rows, const int32_t* __restrict__ perm,
+                                                    const int64_t* __restrict__ srp, const int32_t* __restrict__ sci,
+                                                    const int32_t* __restrict__ cmap, const int64_t* __restrict__ off,
+                                                    int32_t* __restrict__ rp, int32_t* __restrict__ ci) {
+    for (int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x; r <= rows; r += (int64_t)gridDim.x * BLOCK) {
+        rp[r] = (int32_t)off[r];
+        if (r == rows) continue;
+        const int32_t q = perm[r];
+        if (q < 0) continue;
+        for (int64_t e = srp[q], o = off[r]; e < srp[q + 1]; ++e, ++o) ci[o] = cmap ? cmap[sci[e]] : sci[e];
+    }
+}
+
+// values: transposed source, row scale by the source column (= the original row of A)
+__global__ __launch_bounds__(BLOCK) void k_c32_vals(int64_t rows, const int32_t* __restrict__ perm,
+                                                    const int64_t* __restrict__ srp, const int32_t* __restrict__ sci,
+                                                    const double* __restrict__ sval, const double* __restrict__ rs,
+                                                    const int32_t* __restrict__ rp, double* __restrict__ val) {
+    for (int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BLOCK) {
+        const int32_t q = perm[r];
+        if (q < 0) continue;
+        for (int64_t e = srp[q], o = rp[r]; e < srp[q + 1]; ++e, ++o) val[o] = sval[e] * rs[sci[e]];
+    }
+}
+
+void build_csr32(Csr32& C, const Csr& src, int64_t rows, const int32_t* cmap, hipStream_t st) {
+    C.rows = rows;
+    DBuf<int64_t> off(rows + 1);
+    off.zero(st);
+    hipLaunchKernelGGL(k_c32_count, dim3(grid_for(rows)), dim3(BLOCK), 0, st, rows, C.perm.p, src.rp.p, off.p);
+    KERNEL_CHECK();
+    C.nnz = exclusive_scan_i64(off.p, rows + 1, st);
+    if (C.nnz >= (int64_t(1) << 31)) throw std::invalid_argument("data part too large for 32-bit offsets");
+    C.rp.alloc(rows + 1);
+    C.ci.alloc(std::max<int64_t>(C.nnz, 1));
+    C.val.alloc(std::max<int64_t>(C.nnz, 1));
+    hipLaunchKernelGGL(k_c32_fill, dim3(grid_for(rows + 1)), dim3(BLOCK), 0, st, rows, C.perm.p, src.rp.p, src.ci.p,
+                       cmap, off.p, C.rp.p, C.ci.p);
+    KERNEL_CHECK();
+    HIP_CHECK(hipStreamSynchronize(st));
+}
+
 // Data rows of a structured system: Ad (SELL rows = data rows by first column, full column ids)
 // and ATd (SELL rows = node-enumeration positions, column ids = Ad row positions).
 void build_stencil_operator(System& S) {
@@ -589,7 +639,7 @@ void build_stencil_operator(System& S) {
     hipLaunchKernelGGL(k_enum_perm, dim3(grid_for(ne)), dim3(BLOCK), 0, st, S.mfd.p, ne,
                        S.have_colmap ? S.colmap.p : nullptr, S.ATd.perm.p);
     KERNEL_CHECK();
-    build_sell(S.ATd, S.GdT, ne, inv.p, st);
+    build_csr32(S.ATd, S.GdT, ne, inv.p, st);
     S.csf.alloc(std::max<int64_t>(nf, 1));
     S.zv.alloc(std::max<int64_t>(nf, 1));
     S.zv.zero(st);
@@ -667,8 +717,8 @@ void scaling_fill_values(System& S, int precond, bool set_csf) {
         hipLaunchKernelGGL(k_sell_vals, dim3(grid_for(npts)), dim3(BLOCK), 0, st, npts, S.G.rp.p, S.G.ci.p,
                            S.G.val.p, S.rs.p, nullptr, 0, S.Ad.perm.p, S.Ad.sp.p, S.Ad.val.p);
         KERNEL_CHECK();
-        hipLaunchKernelGGL(k_sell_vals, dim3(grid_for(S.ATd.rows)), dim3(BLOCK), 0, st, S.ATd.rows, S.GdT.rp.p,
-                           S.GdT.ci.p, S.GdT.val.p, S.rs.p, nullptr, 1, S.ATd.perm.p, S.ATd.sp.p, S.ATd.val.p);
+        hipLaunchKernelGGL(k_c32_vals, dim3(grid_for(S.ATd.rows)), dim3(BLOCK), 0, st, S.ATd.rows, S.ATd.perm.p,
+                           S.GdT.rp.p, S.GdT.ci.p, S.GdT.val.p, S.rs.p, S.ATd.rp.p, S.ATd.val.p);
         KERNEL_CHECK();
         if (set_csf) {   // distributed ranks assemble csf themselves (column norms span ranks)
             S.csf.zero(st);
@@ -734,7 +784,7 @@ void relabel_columns(System& S, const int32_t* h_map, int64_t n_local) {
     S.GT = Csr{};
     S.mf = false;   // distributed ranks stream the assembled local operator
     S.Ad = Sell{};
-    S.ATd = Sell{};
+    S.ATd = Csr32{};
     S.GdT = Csr{};
     finish_formation(S);
 }

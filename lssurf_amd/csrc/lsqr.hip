@@ -371,6 +371,7 @@ Grids grids_for(const System& S) {
     Grids g;
     g.gD = g.gS = g.gM = g.gXf = 1;
     g.gB = grid_for(std::max<int64_t>(S.nblk, 1), BLOCK, NPART);
+
     if (S.mf) {
         g.gD = (int)std::min<int64_t>(std::max<int64_t>((S.Ad.nslices + 3) / 4, 1), NPART / 4);
         g.gS = (int)std::min<int64_t>(std::max<int64_t>(S.mfh.nodes / MF_ALIGN, 1), NPART - g.gD);
@@ -452,14 +453,14 @@ void launch_iteration_mf(System& S, const Grids& g, int p, int precond) {
     hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gD + g.gS, S.part_b.p, 0, 0,
                        nullptr);
     if (precond == 3) {   // raw Aᵀũ, then ṽ' = M^T t/β − βṽ/α and zv = M ṽ' per column block
-        hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.sp.p, S.ATd.ci.p, S.ATd.val.p,
+        hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.rp.p, S.ATd.ci.p, S.ATd.val.p,
                            S.mfd.p, S.u.p, S.rs.p, S.csf.p, vt, S.tt.p, S.zv.p, S.part_v.p, 1);
         launch_block_epi(S, true, g.gB, S.tt.p, vt, vo, S.zv.p);
         hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gB, S.part_w.p, g.gXf, 0,
                            nullptr);
         return;
     }
-    hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.sp.p, S.ATd.ci.p, S.ATd.val.p,
+    hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.rp.p, S.ATd.ci.p, S.ATd.val.p,
                        S.mfd.p, S.u.p, S.rs.p, S.csf.p, vt, vo, S.zv.p, S.part_v.p, 0);
     hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gM, S.part_w.p, g.gXf, 0, nullptr);
 }
@@ -531,13 +532,13 @@ void lsqr_init_mf(System& S, const double* h_b, const double* h_x0, const lsq_op
     if (o.precond == 3) {
         S.vb0.zero(st);   // columns outside every block (removed by Ip_c) stay 0
         S.zv.zero(st);
-        hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.sp.p, S.ATd.ci.p, S.ATd.val.p,
+        hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.rp.p, S.ATd.ci.p, S.ATd.val.p,
                            S.mfd.p, S.u.p, S.rs.p, S.csf.p, S.vb1.p, S.tt.p, S.zv.p, S.part_v.p, 1);
         launch_block_epi(S, true, g.gB, S.tt.p, S.vb1.p, S.vb0.p, S.zv.p);
         hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gB, S.part_w.p, g.gXf, 1,
                            nullptr);
     } else {
-        hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.sp.p, S.ATd.ci.p, S.ATd.val.p,
+        hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.rp.p, S.ATd.ci.p, S.ATd.val.p,
                            S.mfd.p, S.u.p, S.rs.p, S.csf.p, S.vb1.p, S.vb0.p, S.zv.p, S.part_v.p, 0);
         hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gM, S.part_w.p, g.gXf, 1,
                            nullptr);
@@ -668,16 +669,21 @@ void run_batch(System& S, int count, bool use_graph, int precond, bool mf) {
 
 // Algorithmic HBM bytes per launch of the two streaming kernels (DESIGN.md §Byte model).
 // Assembled SELL: x/w+A·v = 12Z + 16m + 48n, Aᵀu = 12Z + 8m + 16n (Z = nnz, 12 B per entry).
-// Stencil operator: x/w+A·v = 48 n_f + 12 Z_d + 16 m_d + 24 m_s, Aᵀu = 32 n_f + 12 Z_d + 8 m_d + 16 m_s
-// (Z_d entries of the m_d data rows; m_s stencil rows: rs + u r/w, rs + u; per column y, w r/w,
-// ṽ, zv gathered once / cs, ṽ in, ṽ out, zv out).
+// Stencil operator (n_f full columns, Z_d entries of the m_d data rows, stencil part p with
+// n_p rows): x/w+A·v = 48 n_f + 12 Z_d + 16 m_d + Σ_p n_p (16 + 8 [row scale not constant]);
+// Aᵀu = 36 n_f + 12 Z_d + 8 m_d + Σ_p n_p (8 + 8 [...]).  Per column: y, w read+write, ṽ, zv
+// gathered once / cs, ṽ in, ṽ out, zv out, the 4-B ATd row offset.
 void kernel_bytes(const System& S, bool mf, double out[2]) {
     if (mf) {
-        const double nf = (double)S.n_full, md = (double)S.mfh.npts, ms = (double)(S.G.m - S.mfh.npts);
-        double zd = 0.0;
-        zd = (double)S.GdT.nnz;
-        out[0] = 48.0 * nf + 12.0 * zd + 16.0 * md + 24.0 * ms;
-        out[1] = 32.0 * nf + 12.0 * zd + 8.0 * md + 16.0 * ms;
+        const double nf = (double)S.n_full, md = (double)S.mfh.npts, zd = (double)S.GdT.nnz;
+        double f = 48.0 * nf + 12.0 * zd + 16.0 * md, t = 36.0 * nf + 12.0 * zd + 8.0 * md;
+        for (int p = 0; p < S.mfh.n_parts; ++p) {
+            const double n = (double)S.mfh.p[p].n_eq, w = S.mfh.p[p].wconst ? 0.0 : 8.0;
+            f += n * (16.0 + w);
+            t += n * (8.0 + w);
+        }
+        out[0] = f;
+        out[1] = t;
         return;
     }
     const double Z = (double)S.G.nnz, m = (double)S.G.m, n = (double)S.G.n;
@@ -853,7 +859,7 @@ void lsqr_profile(System& S, int reps, int op, double* out /* [8] */) {
                                        S.y.p, S.w.p, S.vb0.p, S.vb0.p, 1, S.G.m, S.A.nslices, S.A.sp.p, S.A.ci.p,
                                        S.A.val.p, S.u.p, S.part_u.p, S.part_w.p);
                 else if (k == 1 && mf)
-                    hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, S.stream, S.st.p, S.ATd.sp.p,
+                    hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, S.stream, S.st.p, S.ATd.rp.p,
                                        S.ATd.ci.p, S.ATd.val.p, S.mfd.p, S.u.p, S.rs.p, S.csf.p, S.vb0.p, S.vb1.p,
                                        S.zv.p, S.part_v.p, 0);
                 else if (k == 1)

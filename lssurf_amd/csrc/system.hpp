@@ -29,6 +29,14 @@ struct Csr {
     DBuf<double> val;   // nnz
 };
 
+// CSR with int32 offsets whose rows are a permutation of another CSR's rows (perm: row -> source
+// row, -1 = empty); one lane walks one row (ATd: data-row entries of one column)
+struct Csr32 {
+    int64_t rows = 0, nnz = 0;
+    DBuf<int32_t> rp, ci, perm;
+    DBuf<double> val;
+};
+
 struct Sell {
     int64_t rows = 0, nslices = 0, nent = 0;
     DBuf<int64_t> sp;   // nslices+1 entry offsets (multiples of 64)
@@ -121,7 +129,8 @@ struct System {
     bool mf = false;
     MfDesc mfh{};
     DBuf<MfDesc> mfd;
-    Sell Ad, ATd;              // data rows (cols = full ids) / their transpose (rows = node-enumeration positions)
+    Sell Ad;                   // data rows (SELL, column ids = full ids)
+    Csr32 ATd;                 // their transpose: rows = node-enumeration positions, cols = Ad rows
     Csr GdT;                   // transpose of the data rows of G (value source of ATd)
     DBuf<int32_t> keep;        // compact column -> full column
     DBuf<double> csf;          // column scale in the full space (0 = removed column)
