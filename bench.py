@@ -174,6 +174,8 @@ def main():
     ap.add_argument('--dist', action='store_true', help='use the distributed (RCCL) path even at N=1')
     ap.add_argument('--no-pmc', action='store_true', help='skip the rocprofv3 PMC traffic passes')
     ap.add_argument('--op', type=int, default=0, help='0: auto (structured stencil operator), 1: assembled SELL')
+    ap.add_argument('--same-device', action='store_true',
+                    help='testing only: every rank on device 0 (RCCL over loopback sockets, distinct host ids)')
     ap.add_argument('--precond', type=int, default=1,
                     help='1: column scaling, 3: block-Jacobi per (y,x) node (single GPU)')
     ap.add_argument('--pmc-child', action='store_true', help=argparse.SUPPRESS)
@@ -190,8 +192,14 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group('gloo', init_method='env://')
+        from lssurf_amd.dist import _quiet_stdout   # gloo announces its peers on stdout
+        _quiet_stdout(lambda: dist.init_process_group('gloo', init_method='env://'))
 
+    if args.same_device:   # RCCL refuses two ranks on one device of one host
+        os.environ['NCCL_HOSTID'] = f'lsq-bench-host-{rank}'
+        os.environ.setdefault('NCCL_SOCKET_IFNAME', 'lo')
+        os.environ.setdefault('NCCL_IB_DISABLE', '1')
+        local = 0
     if world > 1 or args.dist:
         ds, rhs, w, setup = build_dist_system(args.config, rank, world, local)
         solver = _Dist(ds)
@@ -265,8 +273,9 @@ def main():
             'data': 'synthetic (SURVEY.md §8(d) point cloud)',
             'config': {'workload': f'smooth_fit LSQR, {args.config}', 'rank0_system': info, 'rows': gm, 'cols': gn,
                        'nnz': gZ, 'precond': {1: 'column scaling', 3: 'block-Jacobi per (y,x) node'}.get(args.precond, args.precond),
-                       'operator': 'structured stencil rows + SELL data rows' if info.get('stencil_op') and args.op == 0
-                       and not isinstance(solver, _Dist) else 'assembled SELL',
+                       'operator': 'structured stencil rows + SELL data rows'
+                       if (fs.structured if isinstance(solver, _Dist) else info.get('stencil_op') and args.op == 0)
+                       else 'assembled SELL',
                        'parallelism': f'y-slab rows x{world} (RCCL)' if world > 1 or args.dist else 'single'},
             'device_iter_ms': 1e3 * t_dev / args.steps,
             'hbm_gbs_iter': bytes_iter * args.steps / t_dev / 1e9,
