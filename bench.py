@@ -162,6 +162,21 @@ def pmc_child(config, op):
     fs.close()
 
 
+def e2e(config, iters):
+    """smooth_fit end to end (host assembly, device formation, editing loop, outputs) with the
+    library defaults; prints its timing breakdown as one JSON line."""
+    import lssurf_amd as LS
+    from lssurf_amd import synthetic
+    D, kw = synthetic.points(config)
+    t0 = time.time()
+    S = LS.smooth_fit(data=D, VERBOSE=False, max_iterations=iters, **kw)
+    wall = time.time() - t0
+    tim = {k: (v if not isinstance(v, dict) else {kk: vv for kk, vv in v.items() if kk in ('iters', 'istop', 'time_s')})
+           for k, v in S['timing'].items()}
+    print(json.dumps({'config': config, 'max_iterations': iters, 'wall_s': wall, 'timing': tim,
+                      'n_edited': int(np.sum(S['data'].three_sigma_edit == 0))}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -179,7 +194,11 @@ def main():
     ap.add_argument('--precond', type=int, default=1,
                     help='1: column scaling, 3: block-Jacobi per (y,x) node (single GPU)')
     ap.add_argument('--pmc-child', action='store_true', help=argparse.SUPPRESS)
+    ap.add_argument('--e2e', type=int, default=0, metavar='ITERS',
+                    help='instead of the bench line: time smooth_fit end to end with max_iterations=ITERS')
     args = ap.parse_args()
+    if args.e2e:
+        return e2e(args.config, args.e2e)
     if args.pmc_child:
         return pmc_child(args.config, args.op)
     pmc, pmc_note = None, 'skipped (--no-pmc, --dist or N>1)'

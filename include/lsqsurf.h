@@ -197,6 +197,17 @@ int lsq_vgroup_iterate(lsq_vgroup* g, const double* const* b, int64_t iters, con
 const char* lsq_vgroup_last_error(lsq_vgroup* g);
 void lsq_vgroup_destroy(lsq_vgroup* g);
 
+/* ---- outlier editing (RDE.py:10-18, calc_sigma_extra.py:13-44) -----
+ * calc_sigma_extra's bounded search evaluates RDE(r / sqrt(s² + σ²)) 25–30 times per outer
+ * iteration.  lsq_rde_create uploads r and σ once (finite entries only); lsq_rde_order_stats
+ * returns the requested order statistics (0-based ranks) of r / sqrt(s² + σ²), computed exactly
+ * as numpy does, so the caller's percentile interpolation is bit-identical to RDE's. */
+typedef struct lsq_rde lsq_rde;
+lsq_rde* lsq_rde_create(int32_t device, int64_t n, const double* r, const double* sigma);
+int lsq_rde_order_stats(lsq_rde* c, double sigma_extra, int64_t n_idx, const int64_t* idx, double* out);
+const char* lsq_rde_last_error(lsq_rde* c);
+void lsq_rde_destroy(lsq_rde* c);
+
 /* Bench / profiling hooks.  lsq_profile_kernels times each iteration kernel of the operator
  * `op` (lsq_opts.op) in isolation (reps launches each, HIP events on the handle's stream):
  * out8 = {ms of x/w+A·v, ms of Aᵀu, ms of beta reduce, ms of rotation, algorithmic HBM bytes

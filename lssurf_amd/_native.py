@@ -49,6 +49,7 @@ EXPORTS = ['lsq_default_opts', 'lsq_create', 'lsq_destroy', 'lsq_last_error', 'l
            'lsq_get_rinv', 'lsq_dist_unique_id', 'lsq_create_dist', 'lsq_dist_referenced_cols',
            'lsq_dist_set_layout', 'lsq_dist_set_halo', 'lsq_vgroup_create', 'lsq_vgroup_rank', 'lsq_vgroup_solve', 'lsq_vgroup_iterate',
            'lsq_vgroup_last_error', 'lsq_vgroup_destroy',
+           'lsq_rde_create', 'lsq_rde_order_stats', 'lsq_rde_last_error', 'lsq_rde_destroy',
            'tri_upper_solve_csr', 'tri_upper_inv_csr', 'tri_upper_rowrss_csr', 'tri_last_error']
 
 _lib = None
@@ -94,6 +95,10 @@ def load():
         'lsq_vgroup_iterate': ([P, P, i64, P, P], ctypes.c_int),
         'lsq_vgroup_last_error': ([P], ctypes.c_char_p),
         'lsq_vgroup_destroy': ([P], None),
+        'lsq_rde_create': ([i32, i64, P, P], P),
+        'lsq_rde_order_stats': ([P, f64, i64, P, P], ctypes.c_int),
+        'lsq_rde_last_error': ([P], ctypes.c_char_p),
+        'lsq_rde_destroy': ([P], None),
         'tri_upper_solve_csr': ([i32, i64, P, P, P, P, P], ctypes.c_int),
         'tri_upper_inv_csr': ([i32, i64, P, P, P, i64, ctypes.c_float, P, P, P, P], ctypes.c_int),
         'tri_upper_rowrss_csr': ([i32, i64, P, P, P, P], ctypes.c_int),

@@ -83,9 +83,14 @@ class FitSystem:
         self.stats = None
 
     def solve(self, row_weight, data_keep, rhs, x0=None, **opts):
-        keep = np.concatenate([np.asarray(data_keep, dtype=bool), np.ones(self.n_con, dtype=bool)])
-        self.solver.set_row_weight(row_weight)
-        self.solver.set_row_mask(keep)
+        # re-upload only what changed between outer iterations (weights: same array object)
+        if row_weight is not getattr(self, '_w_last', None):
+            self.solver.set_row_weight(row_weight)
+            self._w_last = row_weight
+        dk = np.asarray(data_keep, dtype=bool)
+        if getattr(self, '_keep_last', None) is None or not np.array_equal(dk, self._keep_last):
+            self.solver.set_row_mask(np.concatenate([dk, np.ones(self.n_con, dtype=bool)]))
+            self._keep_last = dk.copy()
         x, self.stats = self.solver.solve(rhs, x0=x0, **opts)
         return x
 
@@ -140,13 +145,15 @@ def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grid
     x = None
     rs_data = None
     timing['lsq_iters'] = 0
+    weight0 = 1. / np.sqrt(E_all ** 2)     # TCinv diagonal, smooth_fit.py:129 (unchanged unless relaxed)
     for iteration in range(args['max_iterations']):
-        E2_plus = E_all ** 2
+        weight = weight0
         if last_iteration and args['sigma_extra_relax']:
             if args['VERBOSE']:
                 print('smooth_fit.iterate_fit: relaxing errors by sigma_extra')
+            E2_plus = E_all ** 2
             E2_plus[0:G_data.shape[0]] += sigma_extra ** 2
-        weight = 1. / np.sqrt(E2_plus)     # TCinv diagonal, smooth_fit.py:129
+            weight = 1. / np.sqrt(E2_plus)
         if args['VERBOSE']:
             print('starting device lsqr solve for iteration %d at %s' % (iteration, ctime()), flush=True)
         tic = time()
@@ -160,12 +167,15 @@ def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grid
         timing['sparseqr_solve'] = time() - tic
         timing['lsq_iters'] += int(system.stats['iters'])
         timing['lsq_last'] = dict(system.stats)
+        tic = time()
         r_data = data.z - system.data_forward(x)
         rs_data = r_data / data.sigma
+        timing['residual'] = timing.get('residual', 0.) + time() - tic
         if last_iteration:
             break
+        tic_edit = time()
         if args.get('sigma_extra_bin_spacing') is None:
-            sigma_extra = calc_sigma_extra(r_data, data.sigma, in_TSE, sigma_extra_masks)
+            sigma_extra = calc_sigma_extra(r_data, data.sigma, in_TSE, sigma_extra_masks, device=args['device'])
         else:
             sigma_extra = calc_sigma_extra_on_grid(data.x, data.y, r_data, data.sigma, in_TSE,
                                                    sigma_extra_masks=sigma_extra_masks,
@@ -212,6 +222,7 @@ def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grid
                 last_iteration = True
         if iteration == args['max_iterations'] - 2:
             last_iteration = True
+        timing['edit'] = timing.get('edit', 0.) + time() - tic_edit
     return m0, sigma_extra, in_TSE, rs_data
 
 
@@ -244,14 +255,25 @@ def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args,
         r_scaled = r / np.sqrt(data.sigma[tse] ** 2 + data.sigma_extra[tse] ** 2)
     else:
         r_scaled = r / data.sigma[tse]
-    Gd = G_data.toCSR()
+    # Gselᵀ·{1, r_scaled², r²} of smooth_fit.py:341-347 as weighted column sums of G_data's
+    # triplets over the kept data rows (no host CSR of the 24 M-entry data operator)
+    rr, cc, vv = G_data.triplets()
+    tse_b = np.asarray(tse).astype(bool).ravel()
+    rows_tse = np.flatnonzero(tse_b)
+    pos = np.full(tse_b.shape, -1)
+    pos[rows_tse] = np.arange(rows_tse.size)
+    sel = tse_b[rr] & (vv != 0)
+    c_sel, v_sel, p_sel = cc[sel], vv[sel], pos[rr[sel]]
+    n_cols = G_data.col_N
+    sums = {'count': np.bincount(c_sel, weights=v_sel, minlength=n_cols),
+            'scaled': np.bincount(c_sel, weights=v_sel * (r_scaled ** 2)[p_sel], minlength=n_cols),
+            'plain': np.bincount(c_sel, weights=v_sel * (r ** 2)[p_sel], minlength=n_cols)}
     for ff in ['dz', 'z0']:
-        Gsel = Gd[:, G_data.TOC['cols'][ff]][tse, :].T
-        count = Gsel.dot(np.ones_like(r)).reshape(grids[ff].shape)
-        m[ff].assign({'count': count})
+        cols = G_data.TOC['cols'][ff]
+        m[ff].assign({'count': sums['count'][cols].reshape(grids[ff].shape)})
         m[ff].count[m[ff].count == 0] = np.nan
-        m[ff].assign({'misfit_scaled_rms': np.sqrt(Gsel.dot(r_scaled ** 2).reshape(grids[ff].shape) / m[ff].count)})
-        m[ff].assign({'misfit_rms': np.sqrt(Gsel.dot(r ** 2).reshape(grids[ff].shape) / m[ff].count)})
+        m[ff].assign({'misfit_scaled_rms': np.sqrt(sums['scaled'][cols].reshape(grids[ff].shape) / m[ff].count)})
+        m[ff].assign({'misfit_rms': np.sqrt(sums['plain'][cols].reshape(grids[ff].shape) / m[ff].count)})
 
 
 def smooth_fit(**kwargs):

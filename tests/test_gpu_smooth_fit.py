@@ -74,3 +74,23 @@ def test_compute_E_matches_reference(gpu_available):
     assert _rel(E['sigma_z0'].sigma_z0, g['E_sigma_z0']) < 1e-7
     assert _rel(E['sigma_dz'].sigma_dz, g['E_sigma_dz']) < 1e-7
     assert _rel(E['sigma_dzdt_lag1'].sigma_dzdt_lag1, g['E_sigma_dzdt_lag1']) < 1e-6
+
+
+@pytest.mark.parametrize('n', [50, 10_007, 2_000_000])
+def test_device_rde_bit_identical(gpu_available, n):
+    """calc_sigma_extra with the device RDE (lsq_rde_*) returns the host result bit for bit,
+    and so does every RDE evaluation of its search."""
+    from lssurf_amd.calc_sigma_extra import DeviceRDE, calc_sigma_extra, RDE
+    rng = np.random.default_rng(n)
+    r = rng.standard_t(3, n) * 0.3
+    sigma = rng.uniform(0.05, 0.2, n)
+    mask = rng.random(n) > 0.05
+    host = calc_sigma_extra(r, sigma, mask)
+    dev = calc_sigma_extra(r, sigma, mask, device=0)
+    np.testing.assert_array_equal(dev, host)
+    d = DeviceRDE(r[mask], sigma[mask], 0)
+    try:
+        for s in (0.0, 1e-3, 0.137, 2.5):
+            assert d(s) == RDE(r[mask] / np.sqrt(s ** 2 + sigma[mask] ** 2))
+    finally:
+        d.close()
