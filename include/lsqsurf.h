@@ -142,6 +142,9 @@ int lsq_solve(lsq_handle* h, const double* b, double* x_inout, const lsq_opts* o
 /* y = G x (trans = 0; x length n, y length m, UNWEIGHTED rows, all rows) or
  * y = Gᵀ x (trans = 1).  G is the formed operator before row weights and row mask. */
 int lsq_spmv(lsq_handle* h, int32_t trans, const double* x, double* y);
+/* Rows [first, first + count) of G x only (e.g. the data rows: z_est / residuals, smooth_fit.py:146
+ * and :662, without moving the constraint rows over PCIe). */
+int lsq_spmv_rows(lsq_handle* h, int64_t first, int64_t count, const double* x, double* y);
 
 /* Bench / profiling hook: run exactly `iters` LSQR iterations on the current system (no early
  * stop), starting from the state left by the previous call (first call initialises from b).

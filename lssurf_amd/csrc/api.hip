@@ -476,6 +476,19 @@ int lsq_spmv(lsq_handle* h, int32_t trans, const double* x, double* y) {
     });
 }
 
+int lsq_spmv_rows(lsq_handle* h, int64_t first, int64_t count, const double* x, double* y) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_spmv_rows: no matrix");
+        if (first < 0 || count < 0 || first + count > S.G.m) return fail(S, "lsq_spmv_rows: rows out of range");
+        lsq::DBuf<double> dx(std::max<int64_t>(S.G.n, 1)), dy(std::max<int64_t>(count, 1));
+        dx.upload(x, S.G.n, S.stream);
+        lsq::csr_spmv_rows(S, first, count, dx.p, dy.p);
+        dy.download(y, count, S.stream);
+        HIP_CHECK(hipStreamSynchronize(S.stream));
+        return 0;
+    });
+}
+
 struct lsq_vgroup {
     std::vector<lsq_handle*> h;
     hipStream_t stream = nullptr;

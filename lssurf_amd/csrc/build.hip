@@ -759,6 +759,13 @@ void csr_spmv(System& S, int trans, const double* dx, double* dy) {
     KERNEL_CHECK();
 }
 
+void csr_spmv_rows(System& S, int64_t first, int64_t count, const double* dx, double* dy) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_csr_spmv, dim3(grid_for(count)), dim3(BLOCK), 0, S.stream, count, S.G.rp.p + first, S.G.ci.p,
+                       S.G.val.p, dx, dy);
+    KERNEL_CHECK();
+}
+
 void referenced_cols(System& S, uint8_t* h_flags) {
     DBuf<uint8_t> f(std::max<int64_t>(S.G.n, 1));
     f.zero(S.stream);

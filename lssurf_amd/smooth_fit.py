@@ -101,7 +101,7 @@ class FitSystem:
 
     def data_forward(self, x):
         """G_data · (Ip_c x), bit-identical to scipy's csr matvec of the reference."""
-        return self.solver.spmv(x)[:self.n_data]
+        return self.solver.spmv_rows(x, 0, self.n_data)
 
     def close(self):
         self.solver.close()
@@ -226,6 +226,14 @@ def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grid
     return m0, sigma_extra, in_TSE, rs_data
 
 
+def _as_slice(idx):
+    """A contiguous ascending index array as a slice (no fancy-indexing copy of 73 M rows)."""
+    idx = np.asarray(idx)
+    if idx.ndim == 1 and idx.size and idx[-1] - idx[0] == idx.size - 1 and np.all(idx[1:] - idx[:-1] == 1):
+        return slice(int(idx[0]), int(idx[-1]) + 1)
+    return idx
+
+
 def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args, ru=None):
     """Output grids and fit statistics (smooth_fit.py:276-352)."""
     z0g, dzg = grids['z0'], grids['dz']
@@ -244,11 +252,12 @@ def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args,
     m['jitter_bias_grids'] = {}
     if ru is None:               # unscaled constraint residuals Gc·m0 (device product when available)
         ru = Gc.toCSR().dot(m0)
-    rc = (1. / Ec) * ru          # TCinv_cov.dot(ru), smooth_fit.py:324-326
     for eq_type in ['d2z_dt2', 'grad2_z0', 'grad2_dzdt', 'grad2_PS']:
         if eq_type in Gc.TOC['rows']:
-            R[eq_type] = np.sum(rc[Gc.TOC['rows'][eq_type]] ** 2)
-            RMS[eq_type] = np.sqrt(np.mean(ru[Gc.TOC['rows'][eq_type]] ** 2))
+            rows = _as_slice(Gc.TOC['rows'][eq_type])
+            rc = (1. / Ec[rows]) * ru[rows]   # TCinv_cov.dot(ru), smooth_fit.py:324-326
+            R[eq_type] = np.sum(rc ** 2)
+            RMS[eq_type] = np.sqrt(np.mean(ru[rows] ** 2))
     tse = data.three_sigma_edit
     r = (data.z - data.z_est)[tse]
     if args['sigma_extra_relax']:

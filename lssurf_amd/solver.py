@@ -181,6 +181,14 @@ class LSQSolver:
         return y
 
 
+    def spmv_rows(self, x, first, count):
+        """Rows [first, first + count) of G x (unweighted)."""
+        x = as_c(x, np.float64)
+        y = np.zeros(int(count))
+        self._check(self._L.lsq_spmv_rows(self._h, int(first), int(count), ptr(x), ptr(y)), 'lsq_spmv_rows')
+        return y
+
+
 # ---- triangular kernels (drop-in signatures of the reference's Cython modules) -------------
 def _tri_csr(R):
     R = sp.csr_matrix(R)
