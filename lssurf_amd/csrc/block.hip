@@ -99,7 +99,7 @@ __global__ __launch_bounds__(BLOCK) void k_block_factor(int64_t nb, const int64_
         for (int j = 0; j < k; ++j)
             for (int i = 0; i <= j; ++i)
                 if (dead[i] || dead[j]) X[pk(i, j)] = 0.0;
-        for (int e = 0; e < npk; ++e) Ri[(int64_t)e * nb + b] = e < k * (k + 1) / 2 ? X[e] : 0.0;
+        for (int e = 0; e < npk; ++e) Ri[b * npk + e] = e < k * (k + 1) / 2 ? X[e] : 0.0;
     }
 }
 

@@ -370,7 +370,7 @@ struct Grids {
 Grids grids_for(const System& S) {
     Grids g;
     g.gD = g.gS = g.gM = g.gXf = 1;
-    g.gB = grid_for(std::max<int64_t>(S.nblk, 1), BLOCK, NPART);
+    g.gB = grid_for(std::max<int64_t>(S.nblk, 1) * 16, BLOCK, NPART);   // 16 lanes per column block
 
     if (S.mf) {
         g.gD = (int)std::min<int64_t>(std::max<int64_t>((S.Ad.nslices + 3) / 4, 1), NPART / 4);
@@ -507,7 +507,7 @@ void lsqr_init_mf(System& S, const double* h_b, const double* h_x0, const lsq_op
         dy0.zero(st);
         dz0.zero(st);
         if (o.precond == 3)   // y0 = M⁻¹ x0 per block, z0 = x0 (full space)
-            hipLaunchKernelGGL(k_block_warm, dim3(grid_for(S.nblk)), dim3(BLOCK), 0, st, S.nblk, S.blk_ptr.p,
+            hipLaunchKernelGGL(k_block_warm, dim3(grid_for(S.nblk)), dim3(BLOCK), 0, st, S.nblk, S.blk_kmax * (S.blk_kmax + 1) / 2, S.blk_ptr.p,
                                S.blk_cols.p, S.blk_full.p, S.blk_Ri.p, dx0.p, dy0.p, dz0.p);
         else
             hipLaunchKernelGGL(k_mf_warm, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, S.keep.p, dx0.p, S.cs.p, dy0.p,
@@ -567,7 +567,7 @@ void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts&
         dy0.alloc(std::max<int64_t>(n, 1));
         dx0.upload(h_x0, n, st);
         if (block) {   // y0 = M⁻¹ x0 per block; the SELL values are unscaled, so A·M·y0 = A x0
-            hipLaunchKernelGGL(k_block_warm, dim3(grid_for(S.nblk)), dim3(BLOCK), 0, st, S.nblk, S.blk_ptr.p,
+            hipLaunchKernelGGL(k_block_warm, dim3(grid_for(S.nblk)), dim3(BLOCK), 0, st, S.nblk, S.blk_kmax * (S.blk_kmax + 1) / 2, S.blk_ptr.p,
                                S.blk_cols.p, S.blk_cols.p, S.blk_Ri.p, dx0.p, dy0.p, S.zt.p);
         } else if (dense) {   // y0 = R x0 ; the SELL values are unscaled, so A·M·y0 = A x0
             hipLaunchKernelGGL(k_gemv_upper, dim3(g.gR), dim3(BLOCK), 0, st, S.dR.p, n, S.dense_ld, dx0.p, nullptr, 2,
@@ -756,7 +756,8 @@ int lsqr_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq
     HIP_CHECK(hipEventRecord(e1, S.stream));
     const int64_t n = S.G.n;
     if (o.precond == 3)   // x = M y, block by block, into compact positions
-        hipLaunchKernelGGL(k_block_x, dim3(grid_for(S.nblk)), dim3(BLOCK), 0, S.stream, S.nblk, S.blk_ptr.p,
+        hipLaunchKernelGGL(k_block_x, dim3(grid_for(S.nblk)), dim3(BLOCK), 0, S.stream, S.nblk,
+                           S.blk_kmax * (S.blk_kmax + 1) / 2, S.blk_ptr.p,
                            S.blk_cols.p, mf ? S.blk_full.p : S.blk_cols.p, S.blk_Ri.p, S.y.p, S.vb1.p);
     else if (mf)
         hipLaunchKernelGGL(k_mf_x, dim3(grid_for(n)), dim3(BLOCK), 0, S.stream, n, S.keep.p, S.y.p, S.csf.p, S.vb1.p);

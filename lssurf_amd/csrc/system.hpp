@@ -138,7 +138,8 @@ struct System {
 
     // block-Jacobi (precond 3): blocks of compact columns (every kept column in exactly one),
     // R_b⁻¹ packed upper-triangular by columns, element e = j(j+1)/2 + i of block b at
-    // blk_Ri[e * nblk + b] (structure of arrays: lanes = blocks read contiguously)
+    // blk_Ri[b * npk + e], npk = kmax(kmax+1)/2 (a block's factor is one contiguous run: the 16
+    // lanes that apply it read it coalesced)
     int64_t nblk = 0;
     int blk_kmax = 0;
     bool blk_user = false;          // blocks came from lsq_set_column_blocks
