@@ -7,8 +7,9 @@
 // z0/dz/epoch coupling of the data rows and the time-derivative constraints is removed exactly;
 // the iteration count then depends on the spatial coupling only.
 //
-// Factorisation: one thread per block.  (AᵀA)_bb entries are merges of two sorted GT rows
-// (deterministic, no atomics), then an in-register Cholesky and triangular inverse.  Columns
+// Factorisation: (AᵀA)_bb with one thread per (block, entry) — a merge of two sorted GT rows
+// (deterministic, no atomics) — then one thread per block for the Cholesky and the triangular
+// inverse, in place.  Columns
 // whose pivot vanishes (empty or dependent inside the block) are dropped: their rows and columns
 // of R_b⁻¹ are zero, so the iteration never moves them (x_j = 0).
 #include <algorithm>
@@ -45,23 +46,36 @@ __device__ double col_dot(const int64_t* __restrict__ trp, const int32_t* __rest
     return s;
 }
 
-__global__ __launch_bounds__(BLOCK) void k_block_factor(int64_t nb, const int64_t* __restrict__ ptr,
+// (AᵀA)_bb, one thread per (block, packed entry): Ri[b·npk + e] ← N_ij (e = j(j+1)/2 + i)
+__global__ __launch_bounds__(BLOCK) void k_block_normal(int64_t nb, int kmax, const int64_t* __restrict__ ptr,
                                                         const int32_t* __restrict__ cols,
                                                         const int64_t* __restrict__ trp,
                                                         const int32_t* __restrict__ tci,
                                                         const double* __restrict__ tval,
-                                                        const double* __restrict__ rs, int kmax,
+                                                        const double* __restrict__ rs, double* __restrict__ N) {
+    const int npk = kmax * (kmax + 1) / 2;
+    const int64_t total = nb * npk;
+    for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < total; q += (int64_t)gridDim.x * BLOCK) {
+        const int64_t b = q / npk;
+        const int e = (int)(q - b * npk);
+        int j = 0;
+        while ((j + 1) * (j + 2) / 2 <= e) ++j;
+        const int i = e - j * (j + 1) / 2;
+        const int64_t b0 = ptr[b];
+        const int k = (int)(ptr[b + 1] - b0);
+        N[q] = j < k ? col_dot(trp, tci, tval, rs, cols[b0 + i], cols[b0 + j]) : 0.0;
+    }
+}
+
+// In place: N_b -> R_b (Cholesky, upper) -> R_b⁻¹, one thread per block
+__global__ __launch_bounds__(BLOCK) void k_block_factor(int64_t nb, const int64_t* __restrict__ ptr, int kmax,
                                                         double* __restrict__ Ri, unsigned long long* ndead) {
     const int npk = kmax * (kmax + 1) / 2;
     for (int64_t b = (int64_t)blockIdx.x * BLOCK + threadIdx.x; b < nb; b += (int64_t)gridDim.x * BLOCK) {
-        const int64_t b0 = ptr[b];
-        const int k = (int)(ptr[b + 1] - b0);
-        int32_t c[KB];
-        for (int i = 0; i < k; ++i) c[i] = cols[b0 + i];
+        const int k = (int)(ptr[b + 1] - ptr[b]);
         double R[KB_PACK];   // N, then R in place (upper, packed by columns)
         double d0[KB];
-        for (int j = 0; j < k; ++j)
-            for (int i = 0; i <= j; ++i) R[pk(i, j)] = col_dot(trp, tci, tval, rs, c[i], c[j]);
+        for (int e = 0; e < k * (k + 1) / 2; ++e) R[e] = Ri[b * npk + e];
         for (int j = 0; j < k; ++j) d0[j] = R[pk(j, j)];
         bool dead[KB];
         // Cholesky by columns: R_ij = (N_ij − Σ_{l<i} R_li R_lj) / R_ii, R_jj = sqrt(N_jj − Σ R_lj²)
@@ -86,7 +100,7 @@ __global__ __launch_bounds__(BLOCK) void k_block_factor(int64_t nb, const int64_
                 R[pk(j, j)] = sqrt(d);
             }
         }
-        // R⁻¹ (upper) in place, column by column from the diagonal up
+        // R⁻¹ (upper) column by column from the diagonal up
         double X[KB_PACK];
         for (int j = 0; j < k; ++j) {
             X[pk(j, j)] = 1.0 / R[pk(j, j)];
@@ -166,8 +180,11 @@ void block_factor(System& S) {
     if (S.blk_Ri.n != (int64_t)npk * S.nblk) S.blk_Ri.alloc((int64_t)npk * S.nblk);
     DBuf<unsigned long long> nd(1);
     nd.zero(S.stream);
+    hipLaunchKernelGGL(k_block_normal, dim3(grid_for(S.nblk * npk)), dim3(BLOCK), 0, S.stream, S.nblk, S.blk_kmax,
+                       S.blk_ptr.p, S.blk_cols.p, S.GT.rp.p, S.GT.ci.p, S.GT.val.p, S.rs.p, S.blk_Ri.p);
+    KERNEL_CHECK();
     hipLaunchKernelGGL(k_block_factor, dim3(grid_for(S.nblk)), dim3(BLOCK), 0, S.stream, S.nblk, S.blk_ptr.p,
-                       S.blk_cols.p, S.GT.rp.p, S.GT.ci.p, S.GT.val.p, S.rs.p, S.blk_kmax, S.blk_Ri.p, nd.p);
+                       S.blk_kmax, S.blk_Ri.p, nd.p);
     KERNEL_CHECK();
     HIP_CHECK(hipStreamSynchronize(S.stream));
     S.blk_valid = true;

@@ -253,13 +253,16 @@ __global__ __launch_bounds__(BLOCK) void k_scatter_cs(int64_t n, const int32_t* 
         csf[keep[j]] = cs[j];
 }
 
-// per stencil part: min and max of the row scale over its rows (block p -> part p)
+// per stencil part: min and max of the row scale over its rows; blockIdx = (part, chunk of
+// MINMAX_CHUNKS), one (min, max) pair per block, combined on the host
+constexpr int MINMAX_CHUNKS = 64;
 __global__ __launch_bounds__(BLOCK) void k_part_minmax(const MfDesc* __restrict__ d, const double* __restrict__ rs,
                                                        double* __restrict__ out) {
     __shared__ double lo[BLOCK], hi[BLOCK];
-    const MfPart& P = d->p[blockIdx.x];
+    const int p = blockIdx.x / MINMAX_CHUNKS, chunk = blockIdx.x % MINMAX_CHUNKS;
+    const MfPart& P = d->p[p];
     double a = INFINITY, b = -INFINITY;
-    for (int64_t r = threadIdx.x; r < P.n_eq; r += BLOCK) {
+    for (int64_t r = (int64_t)chunk * BLOCK + threadIdx.x; r < P.n_eq; r += (int64_t)MINMAX_CHUNKS * BLOCK) {
         const double x = rs[P.row0 + r];
         a = fmin(a, x);
         b = fmax(b, x);
@@ -688,7 +691,9 @@ void scaling_rows_colnorm(System& S, int precond, bool raw) {
     KERNEL_CHECK();
     S.dense_valid = false;   // the dense and block factors depend on the row scaling
     S.blk_valid = false;
-    if (precond == 1)
+    if (precond == 1 && S.mf)
+        mf_column_scale(S, raw);
+    else if (precond == 1)
         hipLaunchKernelGGL(k_colnorm, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, S.GT.rp.p, S.GT.ci.p, S.GT.val.p,
                            S.rs.p, S.cs.p, raw ? 1 : 0);
     else
@@ -727,15 +732,21 @@ void scaling_fill_values(System& S, int precond, bool set_csf) {
         }
         // parts whose rows share one row scale skip the per-row scale loads in the iteration
         const int np = S.mfh.n_parts;
-        DBuf<double> mm(2 * np);
-        hipLaunchKernelGGL(k_part_minmax, dim3(np), dim3(BLOCK), 0, st, S.mfd.p, S.rs.p, mm.p);
+        const int nc = np * MINMAX_CHUNKS;
+        DBuf<double> mm(2 * nc);
+        hipLaunchKernelGGL(k_part_minmax, dim3(nc), dim3(BLOCK), 0, st, S.mfd.p, S.rs.p, mm.p);
         KERNEL_CHECK();
-        std::vector<double> h(2 * np);
-        mm.download(h.data(), 2 * np, st);
+        std::vector<double> h(2 * nc);
+        mm.download(h.data(), 2 * nc, st);
         HIP_CHECK(hipStreamSynchronize(st));
         for (int p = 0; p < np; ++p) {
-            S.mfh.p[p].wconst = h[2 * p] == h[2 * p + 1] ? 1 : 0;
-            S.mfh.p[p].w = h[2 * p];
+            double lo = INFINITY, hi = -INFINITY;
+            for (int c = 0; c < MINMAX_CHUNKS; ++c) {
+                lo = std::min(lo, h[2 * (p * MINMAX_CHUNKS + c)]);
+                hi = std::max(hi, h[2 * (p * MINMAX_CHUNKS + c) + 1]);
+            }
+            S.mfh.p[p].wconst = lo == hi ? 1 : 0;
+            S.mfh.p[p].w = lo;
         }
         S.mfd.upload(&S.mfh, 1, st);
     }

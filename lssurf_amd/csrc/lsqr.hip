@@ -693,6 +693,17 @@ void kernel_bytes(const System& S, bool mf, double out[2]) {
 
 }  // namespace
 
+// Jacobi column scale of the structured system: squared norms in the full space (scratch: csf),
+// then cs_j = 1/‖A_j‖ (or the squared norm, raw) for the compact columns.
+void mf_column_scale(System& S, bool raw) {
+    hipLaunchKernelGGL(k_mf_colnorm, dim3(grid_for(S.mfh.nodes)), dim3(BLOCK), 0, S.stream, S.mfd.p, S.ATd.perm.p,
+                       S.GdT.rp.p, S.GdT.ci.p, S.GdT.val.p, S.rs.p, S.csf.p);
+    KERNEL_CHECK();
+    hipLaunchKernelGGL(k_norm_gather, dim3(grid_for(S.G.n)), dim3(BLOCK), 0, S.stream, S.G.n, S.keep.p, S.csf.p,
+                       raw ? 1 : 0, S.cs.p);
+    KERNEL_CHECK();
+}
+
 double bytes_per_iter(const System& S, bool mf) {
     double b[2];
     kernel_bytes(S, mf, b);

@@ -212,6 +212,7 @@ void finish_formation(System& S);              // G set -> GT, SELL copies, defa
 void ensure_sell(System& S);                    // assembled A / AT (lazy when S.mf)
 void refresh_scaling(System& S, int precond);   // rs/cs -> SELL values (single GPU)
 void scaling_rows_colnorm(System& S, int precond, bool raw);
+void mf_column_scale(System& S, bool raw);       // lsqr.hip: column norms from the stencil structure
 void scaling_finish_cs(System& S);
 void scaling_fill_values(System& S, int precond, bool set_csf = true);
 bool scaling_stale(const System& S, int precond);
