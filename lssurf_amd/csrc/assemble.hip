@@ -235,6 +235,42 @@ bool describe_stencil_operator(MfDesc& d, int64_t m, int64_t n_full, int32_t n_g
         }
         G.part[G.nparts++] = d.n_parts++;
     }
+    // A·v LDS bands per grid: one per distinct template y offset, spanning its in-row offsets
+    for (int g = 0; g < n_grids; ++g) {
+        MfGrid& G = d.g[g];
+        int emin[2 * MF_R + 1], emax[2 * MF_R + 1], band_of[2 * MF_R + 1];
+        bool used[2 * MF_R + 1] = {};
+        for (int q = 0; q < G.nparts; ++q) {
+            const MfPart& P = d.p[G.part[q]];
+            for (int t = 0; t < P.ntpl; ++t) {
+                const int oy = P.off[t][0] + MF_R, e = P.off[t][1] * G.shape[2] + P.off[t][2];
+                if (!used[oy]) emin[oy] = emax[oy] = e;
+                used[oy] = true;
+                emin[oy] = std::min(emin[oy], e);
+                emax[oy] = std::max(emax[oy], e);
+            }
+        }
+        G.nband = 0;
+        G.lds = 0;
+        for (int oy = 0; oy <= 2 * MF_R; ++oy) {
+            if (!used[oy]) continue;
+            const int b = G.nband++;
+            band_of[oy] = b;
+            G.band_oy[b] = oy - MF_R;
+            G.band_emin[b] = emin[oy];
+            G.band_len[b] = MF_ALIGN + emax[oy] - emin[oy];
+            G.band_start[b] = G.lds;
+            G.lds += G.band_len[b];
+        }
+        if (G.lds > MF_LDS_MAX) G.lds = 0;   // too wide: the A·v kernel gathers from HBM
+        for (int q = 0; q < G.nparts; ++q) {
+            MfPart& P = d.p[G.part[q]];
+            for (int t = 0; t < P.ntpl; ++t) {
+                const int b = band_of[P.off[t][0] + MF_R];
+                P.loff[t] = G.band_start[b] + P.off[t][1] * G.shape[2] + P.off[t][2] - G.band_emin[b];
+            }
+        }
+    }
     // node enumeration: the grids with parts, each starting on a MF_ALIGN boundary, so a block
     // iteration (A·v) or a wave's 256 columns (Aᵀu) never spans two grids; they must cover every
     // column (the Aᵀu kernel walks this enumeration)

@@ -365,12 +365,16 @@ struct Grids {
     int gA, gT, gX, gR, gRT, gE;
     int gD, gS, gM, gXf;   // stencil operator: data-row blocks, node blocks, Aᵀu blocks, x/w blocks
     int gB;                // block-Jacobi epilogue
+    size_t lds;            // dynamic LDS of k_mf_fwd (staged zv bands)
 };
 
 Grids grids_for(const System& S) {
     Grids g;
     g.gD = g.gS = g.gM = g.gXf = 1;
     g.gB = grid_for(std::max<int64_t>(S.nblk, 1) * 16, BLOCK, NPART);   // 16 lanes per column block
+    g.lds = 0;
+    if (S.mf)
+        for (int k = 0; k < S.mfh.n_grids; ++k) g.lds = std::max<size_t>(g.lds, sizeof(double) * S.mfh.g[k].lds);
 
     if (S.mf) {
         g.gD = (int)std::min<int64_t>(std::max<int64_t>((S.Ad.nslices + 3) / 4, 1), NPART / 4);
@@ -447,7 +451,7 @@ void launch_iteration_mf(System& S, const Grids& g, int p, int precond) {
     hipStream_t st = S.stream;
     double* vt = p ? S.vb1.p : S.vb0.p;
     double* vo = p ? S.vb0.p : S.vb1.p;
-    hipLaunchKernelGGL(k_mf_fwd, dim3(g.gXf + g.gD + g.gS), dim3(BLOCK), 0, st, S.st.p, g.gXf, g.gD, S.n_full, S.y.p,
+    hipLaunchKernelGGL(k_mf_fwd, dim3(g.gXf + g.gD + g.gS), dim3(BLOCK), g.lds, st, S.st.p, g.gXf, g.gD, S.n_full, S.y.p,
                        S.w.p, vt, S.mfh.npts, S.Ad.nslices, S.Ad.sp.p, S.Ad.ci.p, S.Ad.val.p, S.mfd.p, S.zv.p, S.rs.p,
                        S.u.p, S.part_u.p, S.part_w.p);
     hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gD + g.gS, S.part_b.p, 0, 0,
@@ -468,7 +472,7 @@ void launch_iteration_mf(System& S, const Grids& g, int p, int precond) {
 // final x/w update of a solve that stopped on the last iteration of a batch (newest ṽ in vb0)
 void launch_flush(System& S, const Grids& g, bool mf) {
     if (mf) {
-        hipLaunchKernelGGL(k_mf_fwd, dim3(g.gXf + g.gD + g.gS), dim3(BLOCK), 0, S.stream, S.st.p, g.gXf, g.gD,
+        hipLaunchKernelGGL(k_mf_fwd, dim3(g.gXf + g.gD + g.gS), dim3(BLOCK), g.lds, S.stream, S.st.p, g.gXf, g.gD,
                            S.n_full, S.y.p, S.w.p, S.vb0.p, S.mfh.npts, S.Ad.nslices, S.Ad.sp.p, S.Ad.ci.p, S.Ad.val.p,
                            S.mfd.p, S.zv.p, S.rs.p, S.u.p, S.part_u.p, S.part_w.p);
         hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, S.stream, S.st.p, S.part_u.p, g.gD + g.gS, S.part_b.p, 0, 0,
@@ -863,7 +867,7 @@ void lsqr_profile(System& S, int reps, int op, double* out /* [8] */) {
             HIP_CHECK(hipEventRecord(e0, S.stream));
             for (int r = 0; r < reps; ++r) {
                 if (k == 0 && mf)
-                    hipLaunchKernelGGL(k_mf_fwd, dim3(g.gXf + g.gD + g.gS), dim3(BLOCK), 0, S.stream, S.st.p, g.gXf,
+                    hipLaunchKernelGGL(k_mf_fwd, dim3(g.gXf + g.gD + g.gS), dim3(BLOCK), g.lds, S.stream, S.st.p, g.gXf,
                                        g.gD, S.n_full, S.y.p, S.w.p, S.vb0.p, S.mfh.npts, S.Ad.nslices, S.Ad.sp.p,
                                        S.Ad.ci.p, S.Ad.val.p, S.mfd.p, S.zv.p, S.rs.p, S.u.p, S.part_u.p, S.part_w.p);
                 else if (k == 0)

@@ -57,6 +57,7 @@ constexpr int MF_MAX_PARTS = 32, MF_MAX_GRID_PARTS = 16, MF_MAX_GRIDS = 4;
 constexpr int MF_NPT = 2;                    // nodes per thread per block iteration
 constexpr int MF_ALIGN = 256 * MF_NPT;       // node-enumeration alignment of every grid
 constexpr int MF_R = 3;                      // |template offset| <= MF_R (8 edge classes per side)
+constexpr int MF_LDS_MAX = 4096;             // doubles of LDS per block for the A·v staging (32 KB)
 struct FastDiv {            // n / d for 0 <= n < 2^31: (n * mul) >> (32 + shift)
     uint64_t mul;
     uint32_t shift, d;
@@ -69,6 +70,7 @@ struct MfPart {
     int32_t doff[8];                         // column offset of template entry t  (Σ off·stride)
     int32_t boff[8];                         // row offset of template entry t     (Σ off·bstride)
     uint64_t mlo[3], mhi[3];                 // template validity masks by edge class (MF_R)
+    int32_t loff[8];                         // A·v: LDS offset of template t (MfGrid bands)
     int32_t wconst, pad;                     // 1: every row of the part has row scale w
     double w;
     double val[8];
@@ -78,6 +80,10 @@ struct MfGrid {
     int32_t shape[3], col0, nodes, node0;    // node0: first position in the MF_ALIGN-aligned enumeration
     FastDiv fd[3];
     int32_t part[MF_MAX_GRID_PARTS];
+    // A·v stages the zv values a block iteration's MF_ALIGN nodes gather in LDS: one band per
+    // distinct template y offset, covering the in-row offsets [emin, emax] of that offset
+    int32_t nband, lds;                      // lds = doubles staged (0: gather from HBM)
+    int32_t band_oy[2 * MF_R + 1], band_emin[2 * MF_R + 1], band_len[2 * MF_R + 1], band_start[2 * MF_R + 1];
 };
 struct MfDesc {
     int32_t n_grids, n_parts;
