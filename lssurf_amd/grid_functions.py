@@ -4,7 +4,10 @@ Host mirror of LSsurf/grid_functions.py:
   setup_grids           :26-134  z0 (y,x) at col 0, dz (y,x,t) at col N_z0, t grid, cell areas
   calc_cell_area        :169-175 (planar; projected areas need pyproj — see below)
   sum_cell_area         :136-167
-  setup_averaging_ops   :209-312 dz/dt lag operators (the avg_scales branch is §8 "next")
+  sym_range             :177-185
+  setup_z0_avg          :187-207 z0 averaged to z0_average_scale
+  setup_averaging_ops   :209-312 dz/dt lag operators, dz and dz/dt averaged over avg_scales
+  setup_avg_mask_ops    :314-324 mean dz, dz/dt over named masks
   validate_by_dz_mask   :346-374
 """
 import warnings
@@ -71,7 +74,20 @@ def sum_cell_area(grid_f, grid_c, cell_area_f=None, return_op=False, sub0s=None,
     return (result, op) if return_op else result
 
 
+def sym_range(N, ni, offset=0.5):
+    """Centre subscripts of averaging cells of ni nodes, symmetric about the grid centre
+    (grid_functions.py:177-185)."""
+    out = np.arange(ni * offset, N / 2, ni)
+    if offset == 0:
+        out = np.r_[-out[-1:0:-1], out] + int(np.floor(N / 2))
+    else:
+        out = np.r_[-out[-1::-1], out] + int(np.floor(N / 2))
+    return np.floor(out[np.abs(out - N / 2) <= N / 2 - ni / 2]).astype(int)
+
+
 def setup_averaging_ops(grid, col_N, args, cell_area=None):
+    """dz/dt at each lag, and dz and dz/dt averaged over ``avg_scales`` (grid_functions.py:209-312).
+    Only the 2-D-mask branches: 3-D (time-varying) masks are outside lssurf_amd."""
     ops = {}
     if args.get('dzdt_lags') is not None:
         if grid.mask_3d is not None:
@@ -82,21 +98,66 @@ def setup_averaging_ops(grid, col_N, args, cell_area=None):
             op.dst_grid.cell_area = grid.cell_area
             op.normalize_by_unit_product()
             ops[name] = op
-    if args.get('avg_scales') and args.get('dzdt_lags') is not None:
-        raise NotImplementedError('setup_averaging_ops: avg_scales averaging ops are the next §8 row')
+    if args.get('avg_scales') is None or args.get('dzdt_lags') is None:
+        return ops
+    n_grid = [c.size for c in grid.ctrs]
+    for scale in args['avg_scales']:
+        name = 'avg_dz_' + str(int(scale)) + 'm'
+        kernel_N = np.floor(np.array([scale / d for d in grid.delta[0:2]] + [1])).astype(int)
+        # the largest scale is centred on the grid centre, the others on odd multiples of δ
+        offset = 0 if scale == np.max(args['avg_scales']) else 0.5
+        sub0s = np.meshgrid(sym_range(n_grid[0], kernel_N[0], offset=offset),
+                            sym_range(n_grid[1], kernel_N[1], offset=offset),
+                            np.arange(grid.shape[2], dtype=int), indexing='ij')
+        op = lin_op(grid, name=name, col_N=col_N).sum_to_grid3(kernel_N + 1, sub0s=sub0s, taper=True)
+        op.apply_mask(mask=cell_area)
+        if cell_area is not None:
+            op.normalize_by_unit_product()
+        else:
+            op.v /= (kernel_N[0] * kernel_N[1])
+        op.dst_grid.cell_area = sum_cell_area(grid, op.dst_grid, sub0s=sub0s, cell_area_f=cell_area)
+        ops[name] = op
+        for lag in args['dzdt_lags']:
+            dz_name = 'avg_dzdt_' + str(int(scale)) + 'm' + '_lag' + str(lag)
+            op = lin_op(grid, name=name, col_N=col_N)
+            op.sum_to_grid3(kernel_N + 1, sub0s=sub0s, lag=lag, taper=True).apply_2d_mask(mask=cell_area)
+            if cell_area is not None:
+                # expected number of nonzero entries per node times the per-epoch weight
+                op.normalize_by_unit_product(wt=2 / (lag * grid.delta[2]))
+            else:
+                op.v /= (kernel_N[0] * kernel_N[1])
+            ops[dz_name] = op
     return ops
 
 
 def setup_z0_avg(grids, col_N, args):
-    if args.get('z0_average_scale') is not None:
-        raise NotImplementedError('setup_z0_avg: z0_average_scale is the next §8 row')
-    return {}
+    """z0 averaged to ``z0_average_scale`` (grid_functions.py:187-207)."""
+    if args.get('z0_average_scale') is None:
+        return {}
+    scale = args['z0_average_scale']
+    name = 'avg_z0_' + str(int(scale)) + 'm'
+    g = grids['z0']
+    kernel_N = np.floor(np.array([scale / d for d in g.delta[0:2]])).astype(int)
+    n_grid = [c.size for c in g.ctrs]
+    sub0s = np.meshgrid(*[np.arange(0, n_grid[d] + 1, kernel_N[d]) for d in (0, 1)], indexing='ij')
+    op = lin_op(g, name=name, col_N=col_N).sum_to_grid3(kernel_N + 1, sub0s=sub0s, taper=True,
+                                                       valid_equations_only=False)
+    op.apply_mask(g.cell_area)
+    op.normalize_by_unit_product()
+    return {name: op}
 
 
 def setup_avg_mask_ops(grid, col_N, avg_masks, dzdt_lags):
-    if avg_masks is not None:
-        raise NotImplementedError('setup_avg_mask_ops: avg_masks is the next §8 row')
-    return {}
+    """Mean dz (and dz/dt per lag) over named 2-D masks (grid_functions.py:314-324)."""
+    if avg_masks is None:
+        return {}
+    ops = {}
+    for name, mask in avg_masks.items():
+        ops[name + '_avg_dz'] = lin_op(grid, col_N=col_N, name=name + '_avg_dz').mean_of_mask(mask, dzdt_lag=None)
+        for lag in dzdt_lags:
+            key = name + f'_avg_dzdt_lag{lag}'
+            ops[key] = lin_op(grid, col_N=col_N, name=key).mean_of_mask(mask, dzdt_lag=lag)
+    return ops
 
 
 def validate_by_dz_mask(data, grids, valid_data):

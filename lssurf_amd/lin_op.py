@@ -11,6 +11,7 @@ bit-identical coefficients:
   add / vstack   lin_op.py:134-161, 555-631
   toCSR          lin_op.py:745-753  (drop exact zeros, sum duplicates)
   mask_for_ind0, normalize_by_unit_product, grid_prod, grid_error, update_dst_grid
+  sum_to_grid3, apply_mask, apply_2d_mask, mean_of_mask   lin_op.py:347-488, 669-732 (averaging)
 
 In addition each operator records its *structure* (``parts``): which stencil or interpolation
 generated which rows.  lssurf_amd's device path uses it to know an operator is a pure
@@ -382,6 +383,82 @@ class lin_op:
         for key, val in mask_scale.items():
             out[sampled == key] = val
         return out
+
+    def apply_mask(self, mask=None, row_N=None, time_step_overlap=1):
+        """Multiply every entry by the mask at its node (lin_op.py:693-732).
+
+        The reference walks the CSR row by row; the product is entry-wise, so here it is one
+        gather of the mask on the CSR entries.  Returns the (row, col)-sorted COO of that CSR,
+        explicit zeros included, as the reference does.  ``time_step_overlap`` > 1 belongs to
+        3-D masks, which lssurf_amd does not support."""
+        if time_step_overlap > 1:
+            raise NotImplementedError('apply_mask: time_step_overlap (3-D masks) is outside lssurf_amd')
+        if mask is None:
+            mask = self.grid.mask
+        mask = np.asarray(mask)
+        A = self.toCSR(row_N=row_N, col_N=self.col_N).tocoo()
+        subs = np.unravel_index(A.col - self.grid.col_0, tuple(self.grid.shape))
+        A.data = A.data * mask.ravel()[np.ravel_multi_index(list(subs[0:mask.ndim]), mask.shape)]
+        self.r, self.c, self.v = A.row, A.col, A.data
+        return self
+
+    def apply_2d_mask(self, mask=None):
+        """apply_mask with a mask on the first two grid dimensions (lin_op.py:669-691)."""
+        if mask is None:
+            mask = self.grid.mask
+        mask = np.asarray(mask)
+        A = self.toCSR().tocoo()
+        subs = np.unravel_index(A.col - self.grid.col_0, tuple(self.grid.shape))
+        A.data = A.data * mask.ravel()[np.ravel_multi_index([subs[0], subs[1]], mask.shape)]
+        self.r, self.c, self.v = A.row, A.col, A.data
+        return self
+
+    def mean_of_mask(self, mask, dzdt_lag=None):
+        """Area-weighted mean over a 2-D mask (per epoch, or its dz/dt at ``dzdt_lag``),
+        lin_op.py:347-402.  ``mask`` is a grid container with ``interp(x, y)``."""
+        g = self.grid
+        yy, xx = np.meshgrid(g.ctrs[0], g.ctrs[1], indexing='ij')
+        mask_g = np.asarray(mask.interp(xx, yy), dtype=float)
+        mask_g[~np.isfinite(mask_g)] = 0
+        i0, j0 = np.nonzero(mask_g)
+        nz = np.flatnonzero(mask_g)
+        w = mask_g if g.cell_area is None else mask_g * g.cell_area
+        v0 = w.ravel()[nz]
+        v0 /= v0.sum()
+        y0 = np.sum((g.bds[0][0] + i0.ravel() * g.delta[0]) * v0)
+        x0 = np.sum((g.bds[1][0] + j0.ravel() * g.delta[1]) * v0)
+        if len(g.shape) < 3:
+            # the reference's 2-D branch fails on a misspelt attribute (lin_op.py:374); the
+            # single-row operator it means to build is built here
+            self.r, self.c, self.v = np.zeros_like(i0), g.global_ind([i0, j0]), v0
+            self.N_eq = 1
+            self.col_N = np.max(self.c) + 1
+            self.__update_size_and_shape__()
+            self.dst_grid = fd_grid([[y0, y0], [x0, x0]], g.delta, 0, col_N=0, srs_proj4=g.srs_proj4)
+            self.dst_ind0 = np.array([0]).astype(int)
+            return self
+        nt = int(g.shape[2])
+        rr, cc, vv = [], [], []
+        if dzdt_lag is None:
+            for k in range(nt):
+                rr.append(np.zeros_like(i0) + k)
+                cc.append(g.global_ind([i0, j0, np.zeros_like(i0) + k]))
+                vv.append(v0)
+            t_vals = g.ctrs[2]
+        else:
+            for k in range(nt - dzdt_lag):
+                for d_lag in (0, dzdt_lag):
+                    rr.append(np.zeros_like(i0) + k)
+                    cc.append(g.global_ind([i0, j0, np.zeros_like(i0) + k + d_lag]))
+                    vv.append(-v0 / dzdt_lag / g.delta[2] if d_lag == 0 else v0 / d_lag / g.delta[2])
+            t_vals = g.ctrs[-1][:-dzdt_lag] + g.delta[-1] * dzdt_lag / 2
+        self.r, self.c, self.v = [np.concatenate(a) for a in (rr, cc, vv)]
+        self.dst_grid = fd_grid([[y0, y0], [x0, x0], [t_vals[0], t_vals[-1]]], g.delta, 0,
+                                col_N=self.r.max() + 1, srs_proj4=g.srs_proj4)
+        self.N_eq = self.r.max() + 1
+        self.__update_size_and_shape__()
+        self.dst_ind0 = np.arange(self.N_eq, dtype=int)
+        return self
 
     def normalize_by_unit_product(self, wt=1):
         absop = lin_op(col_N=self.col_N)

@@ -50,7 +50,7 @@ DEFAULTS = {'reference_epoch': 0, 'W_ctr': 1e4, 'return_fit_objects': False, 'ma
             'lsq_precond': 'auto', 'lsq_dense_max': 16384, 'lsq_warm_start': True}
 
 OUT_OF_SCOPE = ('bias_params', 'sensor_grid_bias_params', 'prior_args', 'prior_edge_args', 'lagrangian_coords',
-                'constraint_scaling_maps', 'mask_file', 'avg_masks', 'z0_average_scale', 'bias_edit_vals')
+                'constraint_scaling_maps', 'mask_file', 'bias_edit_vals')
 
 
 class FitSystem:
@@ -297,8 +297,6 @@ def smooth_fit(**kwargs):
             raise NotImplementedError(f'smooth_fit: {key!r} is outside lssurf_amd (SURVEY.md §2)')
     if args.get('data_slope_sensors') is not None and len(args['data_slope_sensors']) > 0:
         raise NotImplementedError("smooth_fit: 'data_slope_sensors' is outside lssurf_amd")
-    if args.get('avg_scales'):
-        raise NotImplementedError("smooth_fit: 'avg_scales' averaging products are the next §8 row")
     if args.get('sigma_extra_keys') is not None:
         raise NotImplementedError("smooth_fit: 'sigma_extra_keys' is outside lssurf_amd")
 
@@ -389,6 +387,8 @@ def smooth_fit(**kwargs):
             RMS['data'] = np.sqrt(np.mean(r_data ** 2))
         else:
             averaging_ops = setup_averaging_ops(grids['dz'], grids['dz'].col_N, args, grids['dz'].cell_area)
+            averaging_ops.update(setup_z0_avg(grids, grids['dz'].col_N, args))
+            averaging_ops.update(setup_avg_mask_ops(grids['dz'], G_data.col_N, args['avg_masks'], args['dzdt_lags']))
         if args['compute_E']:
             from .errors import calc_and_parse_errors
             if 'sigma_extra' not in data.fields:

@@ -26,7 +26,13 @@ def golden_csr(g, prefix='A'):
 
 def golden_points(g):
     from lssurf_amd import containers as pc
-    return pc.data().from_dict({k[3:]: g[k] for k in g.files if k.startswith('in_')})
+    return pc.data().from_dict({k[3:]: g[k] for k in g.files if k.startswith('in_') and not k.startswith('in_mask_')})
+
+
+def golden_avg_masks(g):
+    """the named avg_masks region of sys_avg.npz as a grid container"""
+    from lssurf_amd import containers as pc
+    return {'basin': pc.grid.data().from_dict({'x': g['in_mask_x'], 'y': g['in_mask_y'], 'z': g['in_mask_z']})}
 
 
 def golden_kwargs(g):

@@ -21,6 +21,12 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 REF = '/root/reference'
 CALLS = []          # (A_coo, b) recorded for every sparseqr.solve call
+RZ_CALLS = []       # A recorded for every sparseqr.rz call (compute_E)
+
+
+def sp_csr(A):
+    import scipy.sparse as sp
+    return sp.csr_matrix(A).copy()
 
 
 class _PcData:
@@ -76,7 +82,20 @@ class _PcData:
 
 
 class _PcGrid(_PcData):
-    pass
+    def interp(self, x, y, gridded=False, field='z'):
+        """bilinear interpolation on the node lattice (x, y vectors); NaN outside.  The
+        averaging-mask fixtures sample it at its own nodes, where any bilinear scheme is exact."""
+        z = np.asarray(getattr(self, field), float)
+        gx, gy = np.asarray(self.x, float), np.asarray(self.y, float)
+        x, y = np.asarray(x, float), np.asarray(y, float)
+        fx, fy = np.interp(x, gx, np.arange(gx.size)), np.interp(y, gy, np.arange(gy.size))
+        i = np.clip(np.floor(fy).astype(int), 0, gy.size - 2)
+        j = np.clip(np.floor(fx).astype(int), 0, gx.size - 2)
+        a, b = fy - i, fx - j
+        out = (z[i, j] * (1 - a) * (1 - b) + z[i + 1, j] * a * (1 - b) + z[i, j + 1] * (1 - a) * b
+               + z[i + 1, j + 1] * a * b)
+        out[(x < gx[0]) | (x > gx[-1]) | (y < gy[0]) | (y > gy[-1])] = np.nan
+        return out
 
 
 def install():
@@ -104,7 +123,11 @@ def install():
         CALLS.append((A.tocsr().copy(), np.array(b, dtype=float).copy()))
         return dense.ls_solve_dense(A, b)
     sq.solve = solve
-    sq.rz = lambda A, b: dense.rz_dense(A, b)
+
+    def rz(A, b):
+        RZ_CALLS.append(sp_csr(A))
+        return dense.rz_dense(A, b)
+    sq.rz = rz
 
     # reference Cython kernels (built from /root/reference/LSsurf/*.pyx by oracle/build_ref.sh)
     np.float = float   # propagate_qz_errors.pyx:7 / spsolve_tr_upper.pyx:6 use the removed alias

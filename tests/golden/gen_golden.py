@@ -18,6 +18,7 @@ sys_*.npz      for each smooth_fit / lin_op configuration: the input points, the
                sigma_extra, dzdt_lag1, E sigma grids)
 tri.npz        I/O of the reference Cython kernels inv_tr_upper / propagate_qz_errors /
                spsolve_tr_upper on random upper-triangular CSR matrices (incl. overflow)
+sys_avg.npz    averaging products (avg_scales, z0_average_scale, avg_masks) and their errors
 kat.npz        the analytic amplitude KAT of notebooks/smooth_fit_demo.ipynb cell 8
 """
 import os
@@ -93,7 +94,7 @@ def synth_points(rng, W, ctr, n, with_t=True, outside=0):
     return x, y, t, z
 
 
-def run_sf(LS, stubs, name, data_dict, sf_kwargs, n_outliers=0, rng=None):
+def run_sf(LS, stubs, name, data_dict, sf_kwargs, n_outliers=0, rng=None, extra=None):
     import pointCollection as pc
     data = pc.data().from_dict(data_dict)
     stubs.CALLS.clear()
@@ -125,13 +126,22 @@ def run_sf(LS, stubs, name, data_dict, sf_kwargs, n_outliers=0, rng=None):
     for f in ['count', 'misfit_rms', 'misfit_scaled_rms']:
         out['z0_' + f] = getattr(m['z0'], f)
         out['dz_' + f] = getattr(m['dz'], f)
+    skip = {'z0', 'dz', 'all', 'extent', 'sensor_bias_grids', 'jitter_bias_grids'}
+    for k in m:
+        if k not in skip and not k.startswith('dzdt_lag'):     # averaging products
+            out['avg_' + k] = np.asarray(getattr(m[k], k))
+            area = np.asarray(getattr(m[k], 'cell_area', None))
+            if area.dtype != object:
+                out['avgarea_' + k] = area
     for k, v in S['R'].items():
         out['R_' + k] = np.array(v)
     for k, v in S['RMS'].items():
         out['RMS_' + k] = np.array(v)
     for k, v in S['E'].items():
         out['E_' + k] = np.asarray(getattr(v, k))
-    out['kwargs'] = np.array(repr({k: v for k, v in sf_kwargs.items()}))
+    out['kwargs'] = np.array(repr({k: v for k, v in sf_kwargs.items() if k != 'avg_masks'}))
+    for k, v in (extra or {}).items():
+        out['in_' + k] = np.asarray(v)
     np.savez_compressed(os.path.join(HERE, f'sys_{name}.npz'), **out)
     print(f'{name}: A {A.shape} nnz {A.nnz}, solves {len(stubs.CALLS)}, opt {out["x_opt"]:.2e}')
 
@@ -174,6 +184,52 @@ def gen_systems(LS, stubs):
                                           spacing={'z0': 100, 'dz': 200, 'dt': 0.25}, E_RMS=E,
                                           reference_epoch=4, max_iterations=1, compute_E=True,
                                           VERBOSE=False, dzdt_lags=[1]))
+
+
+def gen_avg(LS, stubs):
+    """Averaging products (grid_functions.py:177-324, lin_op.py:347-488,669-732):
+    avg_scales (dz and dz/dt per lag), z0_average_scale and a named avg_masks region, with
+    compute_E so their error grids (grid_error) are pinned too."""
+    import pointCollection as pc
+    rng = np.random.default_rng(20251122)
+    W = {'x': 2000., 'y': 2000., 't': 1.25}
+    ctr = {'x': 0., 'y': 0., 't': 0.}
+    x, y, t, z = synth_points(rng, W, ctr, 1500)
+    mx = np.arange(-1000., 1001., 100.)
+    my = np.arange(-1000., 1001., 100.)
+    mz = ((np.abs(my[:, None] - 200.) < 450.) & (np.abs(mx[None, :] + 100.) < 650.)).astype(float)
+    mask = pc.grid.data().from_dict({'x': mx, 'y': my, 'z': mz})
+    run_sf(LS, stubs, 'avg', {'x': x, 'y': y, 'time': t, 'z': z, 'sigma': np.full(x.size, 0.1)},
+           dict(W=W, ctr=ctr, spacing={'z0': 100., 'dz': 100., 'dt': 0.25}, E_RMS=E_RMS_NB,
+                reference_epoch=2, max_iterations=1, VERBOSE=False, dzdt_lags=[1, 2],
+                avg_scales=[400., 1000.], z0_average_scale=400., avg_masks={'basin': mask},
+                compute_E=True),
+           extra={'mask_x': mx, 'mask_y': my, 'mask_z': mz})
+    # the same error grids with an EXACT R⁻¹ (the reference's inv_tr_upper drops |x| <= 1e-5):
+    # R = chol(AᵀA) of the matrix the reference handed to sparseqr.rz, pushed through the
+    # reference's own averaging operators and grid_error
+    import scipy.linalg as sla
+    from LSsurf.constraint_functions import build_reference_epoch_matrix
+    from LSsurf.grid_functions import setup_averaging_ops, setup_avg_mask_ops, setup_z0_avg
+    A = stubs.RZ_CALLS[-1]
+    R = sla.cholesky((A.T @ A).toarray(), lower=False)
+    Rinv = sla.solve_triangular(R, np.eye(R.shape[0]), lower=False)
+    kw = dict(W=W, ctr=ctr, spacing={'z0': 100., 'dz': 100., 'dt': 0.25}, E_RMS=E_RMS_NB, reference_epoch=2,
+              max_iterations=1, VERBOSE=False, dzdt_lags=[1, 2], avg_scales=[400., 1000.],
+              z0_average_scale=400., avg_masks={'basin': mask})
+    F = LS.smooth_fit(data=pc.data().from_dict({'x': x, 'y': y, 'time': t, 'z': z, 'sigma': np.full(x.size, 0.1)}),
+                      return_fit_objects=True, **kw)
+    grids = F['grids']
+    Ip_c = build_reference_epoch_matrix(F['G_data'], F['Gc'], grids, 2)
+    full = sp.csr_matrix(Ip_c.dot(sp.csr_matrix(Rinv)))
+    ops = setup_averaging_ops(grids['dz'], grids['dz'].col_N, kw, grids['dz'].cell_area)
+    ops.update(setup_z0_avg(grids, grids['dz'].col_N, kw))
+    ops.update(setup_avg_mask_ops(grids['dz'], F['G_data'].col_N, kw['avg_masks'], kw['dzdt_lags']))
+    path = os.path.join(HERE, 'sys_avg.npz')
+    out = dict(np.load(path, allow_pickle=False))
+    for k, op in ops.items():
+        out['Eexact_sigma_' + k] = op.grid_error(full)
+    np.savez_compressed(path, **out)
 
 
 def gen_lin2d(LS):
@@ -285,6 +341,7 @@ def main():
     gen_tri(LS)
     gen_lin2d(LS)
     gen_systems(LS, _refstubs)
+    gen_avg(LS, _refstubs)
     gen_kat(LS)
 
 

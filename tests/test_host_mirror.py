@@ -124,3 +124,50 @@ def test_structured_description_of_smooth_fit_system():
     op = LS.lin_op(S['grids']['dz'], name='dzdt_lag1').dzdt(lag=1)
     op.normalize_by_unit_product()
     assert op.parts is None
+
+
+def _same_grid(a, b, rtol):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    assert a.shape == b.shape
+    np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+    ok = np.isfinite(b)
+    np.testing.assert_allclose(a[ok], b[ok], rtol=rtol, atol=rtol * max(np.max(np.abs(b[ok])), 1e-300))
+
+
+def test_averaging_products_match_reference():
+    """avg_scales / z0_average_scale / avg_masks operators applied to the reference's own
+    solution reproduce the reference's averaging grids and their cell areas
+    (grid_functions.py:177-324, lin_op.py:347-488,669-732)."""
+    from conftest import golden_avg_masks
+    from lssurf_amd.grid_functions import setup_averaging_ops, setup_avg_mask_ops, setup_grids, setup_z0_avg
+    from lssurf_amd.smooth_fit import DEFAULTS
+    g = golden('sys_avg.npz')
+    args = dict(DEFAULTS)
+    args.update(golden_kwargs(g))
+    args['avg_masks'] = golden_avg_masks(g)
+    grids, _ = setup_grids(args)
+    ops = setup_averaging_ops(grids['dz'], grids['dz'].col_N, args, grids['dz'].cell_area)
+    ops.update(setup_z0_avg(grids, grids['dz'].col_N, args))
+    ops.update(setup_avg_mask_ops(grids['dz'], grids['dz'].col_N, args['avg_masks'], args['dzdt_lags']))
+    expect = {k[4:] for k in g.files if k.startswith('avg_')}
+    assert expect == {k for k in ops if not k.startswith('dzdt_lag')}
+    m0 = g['m_all']
+    for k in expect:
+        _same_grid(ops[k].grid_prod(m0), g['avg_' + k], 1e-12)
+        if 'avgarea_' + k in g.files:
+            _same_grid(ops[k].dst_grid.cell_area, g['avgarea_' + k], 1e-12)
+
+
+def test_sym_range_and_z0_avg_bound():
+    """sym_range is symmetric about the centre; a z0 averaging grid whose subscripts reach
+    one past the last node raises, as the reference's ravel_multi_index does."""
+    from lssurf_amd.grid_functions import setup_grids, setup_z0_avg, sym_range
+    from lssurf_amd.smooth_fit import DEFAULTS
+    for N, ni, off in [(21, 4, 0.5), (21, 10, 0), (1025, 10, 0.5), (1024, 25, 0)]:
+        s = sym_range(N, ni, off)
+        assert np.all(np.diff(s) == ni) and s.min() >= 0 and s.max() < N
+    args = dict(DEFAULTS, W={'x': 2000., 'y': 2000., 't': 1.}, ctr={'x': 0., 'y': 0., 't': 0.},
+                spacing={'z0': 100., 'dz': 100., 'dt': .25}, z0_average_scale=300.)
+    grids, _ = setup_grids(args)
+    with pytest.raises(ValueError):
+        setup_z0_avg(grids, grids['dz'].col_N, args)
