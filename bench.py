@@ -82,10 +82,10 @@ class _Dist:
     def info(self):
         return self.ds.info()
 
-    def iterate(self, rhs, iters, op=0, precond=1):
+    def iterate(self, rhs, iters, op=0, precond=1, method=0):
         return self.ds.iterate(None, None, iters)
 
-    def solve(self, rhs, op=0, precond=1):
+    def solve(self, rhs, op=0, precond=1, method=0):
         x = self.ds.solve(None, None)
         return x, self.ds.stats
 
@@ -109,11 +109,13 @@ def cpu_baseline(fs, b_weighted, sample_iters, threads):
                                       f'OpenMP, column-scaled), {st["time_s"]:.1f} s'}
 
 
-# kernel symbols per role: assembled-SELL operator / structured stencil operator
-KERNEL_SYMBOL = {'xw_spmv': ('k_xw_spmv(', 'k_mf_fwd('), 'spmtv': ('k_spmtv(', 'k_mf_spmtv(')}
+# kernel symbols per role: LSQR (assembled-SELL operator / structured stencil operator), CGNR
+KERNEL_SYMBOL = {0: {'xw_spmv': ('k_xw_spmv(', 'k_mf_fwd('), 'spmtv': ('k_spmtv(', 'k_mf_spmtv(')},
+                 1: {'cg_data': ('k_cg_data(',), 'cg_normal': ('k_cg_normal(',),
+                     'cg_update': ('k_cg_block(', 'k_cg_jacobi(')}}
 
 
-def pmc_traffic(config, op, timeout=300):
+def pmc_traffic(config, op, method=0, precond=1, timeout=300):
     """HBM-side bytes per launch of each iteration kernel from rocprofv3 PMC counters, collected in two
     separate passes (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass on gfx950) of a short
     child run of this script.  Units: KiB.  FETCH_SIZE is doubled: on gfx950 it reports exactly
@@ -133,7 +135,8 @@ def pmc_traffic(config, op, timeout=300):
         for ctr in ('FETCH_SIZE', 'WRITE_SIZE'):
             out = os.path.join(tmp, ctr)
             cmd = [exe, '--pmc', ctr, '-d', out, '-o', 'run', '--output-format', 'csv', '--',
-                   sys.executable, os.path.abspath(__file__), '--pmc-child', '--config', config, '--op', str(op)]
+                   sys.executable, os.path.abspath(__file__), '--pmc-child', '--config', config, '--op', str(op),
+                   '--method', ['lsqr', 'cgnr'][method], '--precond', str(precond)]
             try:
                 r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=timeout,
                                    env=dict(os.environ, TMPDIR=tmp))
@@ -142,7 +145,7 @@ def pmc_traffic(config, op, timeout=300):
             if r.returncode != 0:
                 return None, f'rocprofv3 --pmc {ctr} rc={r.returncode}'
             files = [os.path.join(dp, f) for dp, _, fs in os.walk(out) for f in fs if f.endswith('counter_collection.csv')]
-            for kernel, syms in KERNEL_SYMBOL.items():
+            for kernel, syms in KERNEL_SYMBOL[method].items():
                 xs = []
                 for f in files:
                     for row in csv.DictReader(open(f)):
@@ -152,13 +155,13 @@ def pmc_traffic(config, op, timeout=300):
                     return None, f'no {ctr} samples for {kernel}'
                 vals[kernel, ctr] = sum(xs) / len(xs) * 1024.0
     return {k: {'fetch_bytes': 2.0 * vals[k, 'FETCH_SIZE'], 'write_bytes': vals[k, 'WRITE_SIZE'],
-                'total': 2.0 * vals[k, 'FETCH_SIZE'] + vals[k, 'WRITE_SIZE']} for k in KERNEL_SYMBOL}, None
+                'total': 2.0 * vals[k, 'FETCH_SIZE'] + vals[k, 'WRITE_SIZE']} for k in KERNEL_SYMBOL[method]}, None
 
 
-def pmc_child(config, op):
+def pmc_child(config, op, method, precond):
     """Short run under the profiler: formation + a few iterations of each kernel."""
     fs, rhs, w, _ = build_system(config, 0)
-    fs.solver.iterate(rhs, 4, op=op)
+    fs.solver.iterate(rhs, 4, op=op, method=method, precond=precond)
     fs.close()
 
 
@@ -191,21 +194,27 @@ def main():
     ap.add_argument('--op', type=int, default=0, help='0: auto (structured stencil operator), 1: assembled SELL')
     ap.add_argument('--same-device', action='store_true',
                     help='testing only: every rank on device 0 (RCCL over loopback sockets, distinct host ids)')
-    ap.add_argument('--precond', type=int, default=1,
-                    help='1: column scaling, 3: block-Jacobi per (y,x) node (single GPU)')
+    ap.add_argument('--precond', type=int, default=3,
+                    help='1: column scaling, 3: block-Jacobi per (y,x) node (smooth_fit default at this size)')
+    ap.add_argument('--method', default='cgnr', choices=['cgnr', 'lsqr'],
+                    help='cgnr: PCG on the normal equations, fused normal-stencil operator (smooth_fit default); '
+                         'lsqr: LSQR on the stencil operator')
     ap.add_argument('--pmc-child', action='store_true', help=argparse.SUPPRESS)
     ap.add_argument('--e2e', type=int, default=0, metavar='ITERS',
                     help='instead of the bench line: time smooth_fit end to end with max_iterations=ITERS')
     args = ap.parse_args()
     if args.e2e:
         return e2e(args.config, args.e2e)
-    if args.pmc_child:
-        return pmc_child(args.config, args.op)
-    pmc, pmc_note = None, 'skipped (--no-pmc, --dist or N>1)'
-    if int(os.environ.get('WORLD_SIZE', '1')) == 1 and not args.no_pmc and not args.dist:
-        pmc, pmc_note = pmc_traffic(args.config, args.op)   # child processes, before this one touches the GPU
-
     world = int(os.environ.get('WORLD_SIZE', '1'))
+    if world > 1 or args.dist:   # distributed ranks run LSQR with column scaling
+        args.method, args.precond = 'lsqr', 1
+    meth = 1 if args.method == 'cgnr' else 0
+    if args.pmc_child:
+        return pmc_child(args.config, args.op, meth, args.precond)
+    pmc, pmc_note = None, 'skipped (--no-pmc, --dist or N>1)'
+    if world == 1 and not args.no_pmc and not args.dist:
+        pmc, pmc_note = pmc_traffic(args.config, args.op, meth, args.precond)   # child processes, before this one touches the GPU
+
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     dist = None
@@ -233,10 +242,10 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    solver.iterate(rhs, args.warmup, op=args.op, precond=args.precond)
+    solver.iterate(rhs, args.warmup, op=args.op, precond=args.precond, method=meth)
     barrier()
     t0 = time.perf_counter()
-    st = solver.iterate(rhs, args.steps, op=args.op, precond=args.precond)   # synchronous: returns after the device finished
+    st = solver.iterate(rhs, args.steps, op=args.op, precond=args.precond, method=meth)   # synchronous: returns after the device finished
     barrier()
     t_wall = time.perf_counter() - t0
     t_dev = st['time_s']
@@ -259,28 +268,30 @@ def main():
         gn = int(fs.keep_cols.size)
     bytes_iter = st['bytes_per_iter']
 
-    prof = solver.profile_kernels(reps=10, op=args.op)
+    if meth == 1:
+        prof = solver.profile_cg(reps=10, precond=args.precond)
+        roles = ('cg_data', 'cg_normal', 'cg_update')
+    else:
+        prof = solver.profile_kernels(reps=10, op=args.op)
+        roles = ('spmtv', 'xw_spmv')
     # algorithmic bytes per launch (DESIGN.md §Byte model)
     kb = prof.pop('bytes')   # algorithmic bytes per launch, from the library's byte model
-    dom = max(('spmtv', 'xw_spmv'), key=lambda k: prof[k])
+    dom = max(roles, key=lambda k: prof[k])
     achieved = kb[dom] / (prof[dom] * 1e-3) / 1e9
 
     solve = {}
     if not args.no_solve:
-        # solve wall-time with smooth_fit's default preconditioner for this size (block-Jacobi per
-        # (y, x) node when the system has node blocks), and with the timed iteration's column scaling
-        x, sst = solver.solve(rhs, op=args.op, precond=args.precond)
-        col = {'solve_time_s': sst['time_s'], 'solve_iters': int(sst['iters']), 'solve_istop': int(sst['istop']),
-               'precond': args.precond}
-        if args.precond != 3 and getattr(fs, 'has_blocks', False):
-            x3, s3 = solver.solve(rhs, op=args.op, precond=3)
-            solve = {'solve_time_s': s3['time_s'], 'solve_iters': int(s3['iters']), 'solve_istop': int(s3['istop']),
-                     'solve_precond': 'block-Jacobi per (y,x) node (smooth_fit default)',
-                     'solve_column_scaled': col,
-                     'solve_rel_diff': float(np.linalg.norm(x3 - x) / np.linalg.norm(x))}
-        else:
-            solve = {'solve_time_s': col['solve_time_s'], 'solve_iters': col['solve_iters'],
-                     'solve_istop': col['solve_istop'], 'solve_precond': args.precond}
+        # solve wall-time of the timed configuration (smooth_fit's default: CGNR + block-Jacobi),
+        # and LSQR with the same preconditioner for comparison
+        x, sst = solver.solve(rhs, op=args.op, precond=args.precond, method=meth)
+        solve = {'solve_time_s': sst['time_s'], 'solve_iters': int(sst['iters']), 'solve_istop': int(sst['istop']),
+                 'solve_method': ['lsqr', 'cgnr'][int(sst.get('method', 0))],
+                 'solve_precond': {1: 'column scaling', 3: 'block-Jacobi per (y,x) node'}.get(args.precond, args.precond)}
+        if meth == 1:
+            xl, sl = solver.solve(rhs, op=args.op, precond=args.precond, method=0)
+            solve['solve_lsqr'] = {'solve_time_s': sl['time_s'], 'solve_iters': int(sl['iters']),
+                                   'solve_istop': int(sl['istop'])}
+            solve['solve_rel_diff_vs_lsqr'] = float(np.linalg.norm(x - xl) / np.linalg.norm(xl))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not args.dist:
@@ -289,11 +300,13 @@ def main():
     fs.close()
 
     traffic, traffic_note = (pmc[dom]['total'], pmc) if pmc else (None, pmc_note)
+    method_name = {0: 'LSQR', 1: 'CGNR (PCG on AᵀA)'}[int(st.get('method', meth))]
 
     if rank == 0:
         out = {
             'metric': 'LSQR iters/sec + solve wall-time, 1024x1024x12 grid / 2M pts, 1-8 GPU',
-            'value': value, 'unit': 'LSQR iters/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'value': value, 'unit': 'LSQR iters/s',
+            'solver': method_name, 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': ms_per_step, 'higher_is_better': True,
             'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f64',
             'data': 'synthetic (SURVEY.md §8(d) point cloud)',

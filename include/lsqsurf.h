@@ -42,7 +42,10 @@ typedef struct lsq_handle lsq_handle;
 /* Solver options.  Defaults (lsq_default_opts) reproduce scipy.sparse.linalg.lsqr's stopping
  * rules with atol = btol = 1e-10, conlim = 1e8, maxit = 4*n. */
 typedef struct lsq_opts {
-    int32_t method;        /* 0 = LSQR (Paige & Saunders 1982)                                 */
+    int32_t method;        /* 0 = LSQR (Paige & Saunders 1982); 1 = CGNR: preconditioned CG on  */
+                           /*     the normal equations with the fused normal-stencil operator   */
+                           /*     (structured single-GPU systems, precond 1 or 3; other systems */
+                           /*     fall back to LSQR and report method 0 in lsq_stats)           */
     int32_t precond;       /* 0 = none, 1 = column (Jacobi) scaling, 2 = dense Cholesky R⁻¹   */
                            /*     (exact right preconditioner; n up to a few 10^4), 3 = block-  */
                            /*     Jacobi: R_b⁻¹ of every column block (lsq_set_column_blocks;   */
@@ -61,7 +64,7 @@ typedef struct lsq_opts {
 typedef struct lsq_stats {
     int64_t iters;
     int32_t istop;         /* scipy istop: 1,2 converged; 3 cond limit; 4-6 machine precision; 7 maxit */
-    int32_t reserved;
+    int32_t method;        /* method that ran: 0 LSQR, 1 CGNR (acond is not estimated: 0)      */
     double  r1norm, r2norm, anorm, acond, arnorm, xnorm;
     double  time_s;        /* device-resident iteration time (A, b already in HBM)              */
     double  bytes_per_iter;/* algorithmic HBM bytes of one LSQR iteration (DESIGN.md byte model)*/
@@ -218,6 +221,16 @@ void lsq_rde_destroy(lsq_rde* c);
  * state.  lsq_sell_info: out8 = {m, n, nnz, SELL entries streamed by A·v, by Aᵀu, device bytes
  * of the operator copies, 1 if the structured stencil operator is available, n_full}. */
 int lsq_profile_kernels(lsq_handle* h, int32_t reps, int32_t op, double* out8);
+/* CGNR (method 1) hooks.  lsq_cg_available: 1 when method 1 runs CGNR on this system with this
+ * preconditioner (it builds the normal-stencil tables), 0 when it would fall back to LSQR (the
+ * reason is in lsq_last_error).  lsq_profile_cg: per-kernel HIP-event times of one CG iteration,
+ * out8 = {ms data rows t = Ad·p, ms normal operator q = N p + Adᵀt, ms update + preconditioner,
+ * ms of the two scalar kernels, algorithmic HBM bytes per launch of the first three, 0}.
+ * lsq_normal_apply: q = AᵀA p for the current row weights/mask, p and q over the FULL column
+ * space (length n_full of lsq_set_col_map; test hook for the normal operator). */
+int lsq_cg_available(lsq_handle* h, int32_t precond);
+int lsq_profile_cg(lsq_handle* h, int32_t reps, int32_t precond, double* out8);
+int lsq_normal_apply(lsq_handle* h, const double* p, double* q);
 int lsq_sell_info(lsq_handle* h, int64_t* out8);
 
 /* ---- triangular kernels (replace the Cython kernels; R upper triangular CSR, int32 indices,

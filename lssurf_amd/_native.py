@@ -32,20 +32,20 @@ class StencilDesc(ctypes.Structure):
 
 
 class LsqStats(ctypes.Structure):
-    _fields_ = [('iters', ctypes.c_int64), ('istop', ctypes.c_int32), ('reserved', ctypes.c_int32),
+    _fields_ = [('iters', ctypes.c_int64), ('istop', ctypes.c_int32), ('method', ctypes.c_int32),
                 ('r1norm', ctypes.c_double), ('r2norm', ctypes.c_double), ('anorm', ctypes.c_double),
                 ('acond', ctypes.c_double), ('arnorm', ctypes.c_double), ('xnorm', ctypes.c_double),
                 ('time_s', ctypes.c_double), ('bytes_per_iter', ctypes.c_double)]
 
     def as_dict(self):
-        return {f: getattr(self, f) for f, _ in self._fields_ if f != 'reserved'}
+        return {f: getattr(self, f) for f, _ in self._fields_}
 
 
 # every symbol declared in include/lsqsurf.h
 EXPORTS = ['lsq_default_opts', 'lsq_create', 'lsq_destroy', 'lsq_last_error', 'lsq_set_col_map',
            'lsq_set_matrix_coo', 'lsq_set_matrix_stencil', 'lsq_set_row_weight', 'lsq_set_row_mask',
            'lsq_set_column_blocks', 'lsq_shape', 'lsq_get_csr',
-           'lsq_solve', 'lsq_spmv', 'lsq_spmv_rows', 'lsq_iterate', 'lsq_profile_kernels', 'lsq_sell_info', 'lsq_sigma_x',
+           'lsq_solve', 'lsq_spmv', 'lsq_spmv_rows', 'lsq_iterate', 'lsq_profile_kernels', 'lsq_cg_available', 'lsq_profile_cg', 'lsq_normal_apply', 'lsq_sell_info', 'lsq_sigma_x',
            'lsq_get_rinv', 'lsq_dist_unique_id', 'lsq_create_dist', 'lsq_dist_referenced_cols',
            'lsq_dist_set_layout', 'lsq_dist_set_halo', 'lsq_vgroup_create', 'lsq_vgroup_rank', 'lsq_vgroup_solve', 'lsq_vgroup_iterate',
            'lsq_vgroup_last_error', 'lsq_vgroup_destroy',
@@ -82,6 +82,9 @@ def load():
         'lsq_spmv_rows': ([P, i64, i64, P, P], ctypes.c_int),
         'lsq_iterate': ([P, P, i64, P, P], ctypes.c_int),
         'lsq_profile_kernels': ([P, i32, i32, P], ctypes.c_int),
+        'lsq_cg_available': ([P, i32], ctypes.c_int),
+        'lsq_profile_cg': ([P, i32, i32, P], ctypes.c_int),
+        'lsq_normal_apply': ([P, P, P], ctypes.c_int),
         'lsq_sell_info': ([P, P], ctypes.c_int),
         'lsq_sigma_x': ([P, P], ctypes.c_int),
         'lsq_get_rinv': ([P, P], ctypes.c_int),

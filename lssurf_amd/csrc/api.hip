@@ -8,6 +8,11 @@
 
 namespace lsq {
 int lsqr_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq_stats* stats);
+bool cg_available(System& S, int precond);
+int cg_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq_stats* stats);
+int cg_iterate(System& S, const double* h_b, int64_t iters, const lsq_opts& o, lsq_stats* stats);
+void cg_profile(System& S, int reps, int precond, double* out);
+void cg_apply_normal(System& S, const double* h_p, double* h_q);
 int lsqr_iterate(System& S, const double* h_b, int64_t iters, const lsq_opts& o, lsq_stats* stats);
 void lsqr_profile(System& S, int reps, int op, double* out);
 void lsqr_sigma_x(System& S, double* h_E);
@@ -247,7 +252,7 @@ int lsq_solve(lsq_handle* h, const double* b, double* x_inout, const lsq_opts* o
         lsq_opts d;
         lsq_default_opts(&d);
         if (!o) o = &d;
-        if (o->method != 0) return fail(S, "lsq_solve: only method 0 (LSQR) is implemented");
+        if (o->method != 0 && o->method != 1) return fail(S, "lsq_solve: method must be 0 (LSQR) or 1 (CGNR)");
         if (o->precond < 0 || o->precond > 3) return fail(S, "lsq_solve: precond must be 0, 1, 2 or 3");
         if (S.dist) {
             if (S.virt) return fail(S, "lsq_solve: a virtual rank solves through lsq_vgroup_solve");
@@ -256,6 +261,8 @@ int lsq_solve(lsq_handle* h, const double* b, double* x_inout, const lsq_opts* o
             double* xs[1] = {x_inout};
             return lsq::group_solve(G, &b, xs, *o, s);
         }
+        if (o->method == 1 && lsq::cg_available(S, o->precond)) return lsq::cg_solve(S, b, x_inout, *o, s);
+        if (s) s->method = 0;
         return lsq::lsqr_solve(S, b, x_inout, *o, s);
     });
 }
@@ -272,7 +279,43 @@ int lsq_iterate(lsq_handle* h, const double* b, int64_t iters, const lsq_opts* o
             G.ranks = {&S};
             return lsq::group_iterate(G, &b, iters, *o, s);
         }
+        if (o->method == 1 && lsq::cg_available(S, o->precond)) return lsq::cg_iterate(S, b, iters, *o, s);
+        if (s) s->method = 0;
         return lsq::lsqr_iterate(S, b, iters, *o, s);
+    });
+}
+
+int lsq_cg_available(lsq_handle* h, int32_t precond) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_cg_available: no matrix");
+        if (precond != 1 && precond != 3) {
+            S.err = "CGNR runs with precond 1 (Jacobi) or 3 (block-Jacobi)";
+            return 0;
+        }
+        if (lsq::cg_available(S, precond)) return 1;
+        S.err = S.cg_why.empty() ? "not a structured single-GPU system" : S.cg_why;
+        return 0;
+    });
+}
+
+int lsq_profile_cg(lsq_handle* h, int32_t reps, int32_t precond, double* out8) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_profile_cg: no matrix");
+        if (!out8) return fail(S, "lsq_profile_cg: null output");
+        if (!lsq::cg_available(S, precond)) return fail(S, "lsq_profile_cg: CGNR not available: " + S.cg_why);
+        lsq::graph_cache_drop(&S);
+        lsq::cg_profile(S, reps > 0 ? reps : 10, precond, out8);
+        return 0;
+    });
+}
+
+int lsq_normal_apply(lsq_handle* h, const double* p, double* q) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_normal_apply: no matrix");
+        if (!p || !q) return fail(S, "lsq_normal_apply: null vector");
+        if (!lsq::cg_available(S, 1)) return fail(S, "lsq_normal_apply: no normal-stencil operator: " + S.cg_why);
+        lsq::cg_apply_normal(S, p, q);
+        return 0;
     });
 }
 

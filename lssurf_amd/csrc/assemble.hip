@@ -142,15 +142,6 @@ __global__ __launch_bounds__(BLOCK) void k_gen_rows(int pass, const GenCtx* __re
     }
 }
 
-FastDiv make_fastdiv(uint32_t d) {
-    FastDiv f{};
-    f.d = d;
-    uint32_t s = 0;
-    while ((uint64_t(1) << s) < d) ++s;
-    f.shift = s;
-    f.mul = (uint64_t)(((unsigned __int128)1 << (32 + s)) + d - 1) / d;   // ceil(2^(32+s) / d)
-    return f;
-}
 
 // The structured stencil operator (system.hpp MfDesc) when every part is a clean stencil:
 // every template entry of every centre in the box stays inside its grid, grids do not overlap,

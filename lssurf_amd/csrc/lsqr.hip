@@ -12,6 +12,7 @@
 // of iterations are captured once into a hipGraph and replayed; the host reads the 200-byte
 // state only between batches.  Right preconditioning by column scaling is baked into the SELL
 // values (A·D), and x = D y is applied on the way out.
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <vector>
@@ -633,6 +634,7 @@ struct GraphCache {
     hipGraphExec_t exec = nullptr;
 };
 thread_local GraphCache g_cache;
+thread_local GraphCache g_cache_cg;   // CGNR iteration batches (lsqr_cg.inc)
 
 void launch_any(System& S, const Grids& g, int p, int precond, bool mf) {
     if (mf)
@@ -739,10 +741,11 @@ void prepare(System& S, int precond, bool mf) {
 }  // namespace
 
 void graph_cache_drop(const System* S) {
-    if (g_cache.sys == S && g_cache.exec) {
-        (void)hipGraphExecDestroy(g_cache.exec);
-        g_cache = GraphCache{};
-    }
+    for (GraphCache* c : {&g_cache, &g_cache_cg})
+        if (c->sys == S && c->exec) {
+            (void)hipGraphExecDestroy(c->exec);
+            *c = GraphCache{};
+        }
 }
 
 int lsqr_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq_stats* stats) {
@@ -921,6 +924,8 @@ void lsqr_get_rinv(System& S, double* h_Ri) {
                                hipMemcpyDeviceToHost, S.stream));
     HIP_CHECK(hipStreamSynchronize(S.stream));
 }
+
+#include "lsqr_cg.inc"
 
 #include "lsqr_dist.inc"
 

@@ -62,6 +62,15 @@ struct FastDiv {            // n / d for 0 <= n < 2^31: (n * mul) >> (32 + shift
     uint64_t mul;
     uint32_t shift, d;
 };
+inline FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f{};
+    f.d = d;
+    uint32_t s = 0;
+    while ((uint64_t(1) << s) < d) ++s;
+    f.shift = s;
+    f.mul = (uint64_t)(((unsigned __int128)1 << (32 + s)) + d - 1) / d;   // ceil(2^(32+s) / d)
+    return f;
+}
 struct MfPart {
     int32_t grid, ntpl, row0, n_eq;          // rows [row0, row0 + n_eq) (global row ids < 2^31)
     int32_t lo[3], hi[3], bstride[3];
@@ -108,6 +117,41 @@ struct LsqState {
     int32_t skip_v;     // beta == 0 in the current iteration
     int32_t no_stop;    // lsq_iterate: only maxit stops
     int32_t pad[2];
+};
+
+// CGNR normal operator (lsqr_cg.inc): AᵀA of the stencil rows of one grid is a constant-coefficient
+// stencil whose coefficients depend only on each node's boundary class (position within K_e of
+// either end of dim e, else interior).  Tiles of CG_TX nodes of dim 1 × ty rows of dim 0 × all of
+// dim 2 are staged in LDS with their halo; lane = dim-1 position, so a wave's class is uniform
+// except on tiles at a dim-1 edge.
+constexpr int CG_TX = 64;
+constexpr int CG_MAX_OFF = 64;
+constexpr int CG_MAXI = 16;                 // (row, dim-2) items per wave of one tile
+struct CgGrid {
+    int32_t shape[3], col0, node0;
+    int32_t ty, nty, ntx, tile0;             // tiles of the grid: ids [tile0, tile0 + nty·ntx)
+    int32_t hy, hx, ht, tpad, wx;            // halo per dim, LDS dim-2 stride, LDS dim-1 extent
+    int32_t front, lds;                      // LDS front pad, doubles of the tile image
+    int32_t K[3], ncls[3];                   // boundary classes per dim
+    int32_t noff, coef0;                     // normal-stencil offsets, first coefficient
+    int32_t loff[CG_MAX_OFF];                // LDS offset of each normal-stencil offset
+    FastDiv fd_pad, fd_row;                  // ÷ tpad, ÷ (wx · tpad): staging image index
+    FastDiv fd_s2, fd_int;                   // ÷ shape[2], ÷ (CG_TX · shape[2]): interior index
+};
+struct CgDesc {
+    int32_t n_grids, ntiles, lds_max, pad;
+    CgGrid g[MF_MAX_GRIDS];
+};
+// PCG-on-AᵀA scalar state (device resident).  Quantities are those of CGLS on A·M^{-1/2}; the
+// LSQR estimates (anorm, xnorm of the correction, ‖r‖, ‖Aᵀr‖) follow from the CG scalars through
+// the Lanczos relation.
+struct CgState {
+    double rho, gamma, alpha, beta, alpha_prev, beta_prev;
+    double rn2, bnorm, anorm2, pn2, dp, dn2;
+    double atol, btol;
+    double r1norm, arnorm, xnorm, anorm;
+    int64_t itn, maxit;
+    int32_t istop, stop, no_stop, pad;
 };
 
 struct System {
@@ -181,6 +225,21 @@ struct System {
     bool dist_mf = false;
     DBuf<int32_t> recv_idx;
     DBuf<uint8_t> live;
+
+    // CGNR (method 1): normal-stencil description + coefficient table, rebuilt when the part
+    // row scales change; vectors in the full column space
+    bool cg_ok = false;            // the structured normal operator exists for this system
+    int64_t cg_data_cols = 0;      // columns touched by the data rows
+    std::string cg_why;            // why not (when !cg_ok)
+    CgDesc cgh{};
+    DBuf<CgDesc> cgd;
+    DBuf<double> cg_coef;
+    std::vector<double> cg_wkey;   // part row scales the table was built for
+    DBuf<double> cg_x, cg_s, cg_z, cg_p0, cg_p1, cg_q, cg_t, cg_part_g, cg_part_r;
+    DBuf<CgState> cst;
+    int cg_parity = 0;
+    bool cg_ready = false;         // lsq_iterate state initialised (CG)
+    int cg_mode = -1;
 
     // LSQR workspace
     DBuf<double> u, vb0, vb1, w, y, bw, zt, tt;

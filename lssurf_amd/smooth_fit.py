@@ -47,7 +47,7 @@ DEFAULTS = {'reference_epoch': 0, 'W_ctr': 1e4, 'return_fit_objects': False, 'ma
             # lssurf_amd solver options (new keys; defaults reproduce the exact LS solution to
             # the tolerance documented in DESIGN.md §Parity)
             'device': 0, 'lsq_atol': 1e-12, 'lsq_btol': 1e-12, 'lsq_conlim': 1e12, 'lsq_maxit': 0,
-            'lsq_precond': 'auto', 'lsq_dense_max': 16384, 'lsq_warm_start': True}
+            'lsq_precond': 'auto', 'lsq_dense_max': 16384, 'lsq_warm_start': True, 'lsq_method': 'auto'}
 
 OUT_OF_SCOPE = ('bias_params', 'sensor_grid_bias_params', 'prior_args', 'prior_edge_args', 'lagrangian_coords',
                 'constraint_scaling_maps', 'mask_file', 'bias_edit_vals')
@@ -131,7 +131,11 @@ def _solve_opts(args, n, has_blocks=False):
     if pc_ == 'auto':
         pc_ = 2 if n <= args['lsq_dense_max'] else (3 if has_blocks else 1)
     maxit = args['lsq_maxit'] or (0 if pc_ == 2 else 50 * n)
-    return dict(atol=args['lsq_atol'], btol=args['lsq_btol'], conlim=args['lsq_conlim'], maxit=maxit, precond=pc_)
+    # method 'auto': CGNR (normal-stencil operator, column-space only) with the iterative
+    # preconditioners — the library falls back to LSQR where the structured operator is absent
+    meth = {'auto': 1 if pc_ in (1, 3) else 0, 'lsqr': 0, 'cgnr': 1}[args.get('lsq_method', 'auto')]
+    return dict(atol=args['lsq_atol'], btol=args['lsq_btol'], conlim=args['lsq_conlim'], maxit=maxit, precond=pc_,
+                method=meth)
 
 
 def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grids, sigma_extra_masks=None):

@@ -126,21 +126,25 @@ class LSQSolver:
 
     # ---- solve -------------------------------------------------------------------------------
     def solve(self, b, x0=None, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, batch=16,
-              use_graph=True, op=0):
-        """LSQR; returns (x, stats) with scipy-lsqr-style stats (iters, istop, r1norm, ...)."""
+              use_graph=True, op=0, method=0):
+        """LSQR (method 0) or CGNR (method 1: PCG on the normal equations with the fused
+        normal-stencil operator; LSQR where that operator does not exist — stats['method'] says
+        which ran); returns (x, stats) with scipy-lsqr-style stats (iters, istop, r1norm, ...)."""
         b = as_c(b, np.float64)
         if b.size != self.m:
             raise ValueError(f'b has {b.size} rows, system has {self.m}')
         x = np.zeros(self.n) if x0 is None else as_c(x0, np.float64).copy()
         o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond),
-                         use_x0=int(x0 is not None), batch=int(batch), use_graph=int(bool(use_graph)), op=int(op))
+                         use_x0=int(x0 is not None), batch=int(batch), use_graph=int(bool(use_graph)), op=int(op),
+                         method=int(method))
         st = LsqStats()
         self._check(self._L.lsq_solve(self._h, ptr(b), ptr(x), ctypes.byref(o), ctypes.byref(st)), 'lsq_solve')
         return x, st.as_dict()
 
-    def iterate(self, b, iters, precond=1, batch=16, use_graph=True, op=0):
+    def iterate(self, b, iters, precond=1, batch=16, use_graph=True, op=0, method=0):
         b = as_c(b, np.float64)
-        o = default_opts(precond=int(precond), batch=int(batch), use_graph=int(bool(use_graph)), op=int(op))
+        o = default_opts(precond=int(precond), batch=int(batch), use_graph=int(bool(use_graph)), op=int(op),
+                         method=int(method))
         st = LsqStats()
         self._check(self._L.lsq_iterate(self._h, ptr(b), int(iters), ctypes.byref(o), ctypes.byref(st)),
                     'lsq_iterate')
@@ -154,6 +158,29 @@ class LSQSolver:
         d = dict(zip(['xw_spmv', 'spmtv', 'beta', 'givens'], o[:4].tolist()))
         d['bytes'] = {'xw_spmv': float(o[4]), 'spmtv': float(o[5])}
         return d
+
+    def cg_available(self, precond=3):
+        """(True, '') when method 1 runs CGNR on this system with this preconditioner, else
+        (False, reason) — method 1 then falls back to LSQR."""
+        rc = self._check(self._L.lsq_cg_available(self._h, int(precond)), 'lsq_cg_available')
+        return bool(rc), ('' if rc else self._L.lsq_last_error(self._h).decode())
+
+    def profile_cg(self, reps=20, precond=3):
+        """Per-kernel device time (ms) of one CGNR iteration and algorithmic bytes per launch."""
+        o = np.zeros(8)
+        self._check(self._L.lsq_profile_cg(self._h, int(reps), int(precond), ptr(o)), 'lsq_profile_cg')
+        d = dict(zip(['cg_data', 'cg_normal', 'cg_update', 'cg_scalars'], o[:4].tolist()))
+        d['bytes'] = {'cg_data': float(o[4]), 'cg_normal': float(o[5]), 'cg_update': float(o[6])}
+        return d
+
+    def normal_apply(self, p_full):
+        """q = AᵀA p over the full column space (current weights / mask)."""
+        p = as_c(p_full, np.float64)
+        if p.size != self.n_full:
+            raise ValueError('p must have n_full entries')
+        q = np.zeros(self.n_full)
+        self._check(self._L.lsq_normal_apply(self._h, ptr(p), ptr(q)), 'lsq_normal_apply')
+        return q
 
     def info(self):
         o = np.zeros(8, np.int64)
