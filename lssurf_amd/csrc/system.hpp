@@ -127,6 +127,15 @@ struct LsqState {
 constexpr int CG_TX = 64;
 constexpr int CG_MAX_OFF = 64;
 constexpr int CG_MAXI = 16;                 // (row, dim-2) items per wave of one tile
+// Column mode (every grid: dim 2 ≤ CG_MAXT nodes, |dt| ≤ 2): a thread owns a whole dim-2 column
+// (y, x, 0..S2−1) and accumulates it in registers; the normal stencil is walked as (dy, dx)
+// GROUPS, each reading the neighbour column once from LDS and applying its ≤ 5 dt taps to all
+// S2 outputs.  Coefficients are stored per (cy, cx) class row × group × t (exact t, padded to
+// the template width MAXT with zeros), so the loops are fully unrolled and branch-free.  A
+// workgroup streams a strip of ty rows through an LDS ring (lsqr_cg.inc, cg_strip).
+constexpr int CG_MAXT = 16;
+constexpr int CG_MAX_GRP = 49;
+constexpr int CG_NCOL = 4;                  // ring staging: row-image columns per thread (row image ≤ CG_NCOL·256)
 struct CgGrid {
     int32_t shape[3], col0, node0;
     int32_t ty, nty, ntx, tile0;             // tiles of the grid: ids [tile0, tile0 + nty·ntx)
@@ -135,11 +144,20 @@ struct CgGrid {
     int32_t K[3], ncls[3];                   // boundary classes per dim
     int32_t noff, coef0;                     // normal-stencil offsets, first coefficient
     int32_t loff[CG_MAX_OFF];                // LDS offset of each normal-stencil offset
+    int8_t ooff[CG_MAX_OFF][4];              // the offsets (dy, dx, dt)
     FastDiv fd_pad, fd_row;                  // ÷ tpad, ÷ (wx · tpad): staging image index
     FastDiv fd_s2, fd_int;                   // ÷ shape[2], ÷ (CG_TX · shape[2]): interior index
+    // column mode
+    int32_t maxt, rpw, tq;                   // template column length (1 or CG_MAXT), ring rows per wave and step, -
+    int32_t ngrp[3];                         // groups with max |dt| = 0, 1, 2 (stored in that order)
+    int32_t rowlen, coefc0;                  // coefficients per (cy, cx) class row; first of this grid
+    int32_t gdy[CG_MAX_GRP];                 // dim-0 offset dy of group g
+    int32_t gl[CG_MAX_GRP];                  // in-row LDS offset dx·tpad of group g
+    int32_t gc[CG_MAX_GRP];                  // offset of group g's MAXT × (2·DT_g + 1) coefficients in a row
 };
 struct CgDesc {
-    int32_t n_grids, ntiles, lds_max, pad;
+    int32_t n_grids, ntiles, lds_max, colmode;
+    int32_t nedge, pad[3];                   // column mode: workgroups of k_cg_xedge
     CgGrid g[MF_MAX_GRIDS];
 };
 // PCG-on-AᵀA scalar state (device resident).  Quantities are those of CGLS on A·M^{-1/2}; the
@@ -233,9 +251,9 @@ struct System {
     std::string cg_why;            // why not (when !cg_ok)
     CgDesc cgh{};
     DBuf<CgDesc> cgd;
-    DBuf<double> cg_coef;
+    DBuf<double> cg_coef, cg_coefc;  // class-row tables: offset-major (tile mode), group × t (column mode)
     std::vector<double> cg_wkey;   // part row scales the table was built for
-    DBuf<double> cg_x, cg_s, cg_z, cg_p0, cg_p1, cg_q, cg_t, cg_part_g, cg_part_r;
+    DBuf<double> cg_x, cg_s, cg_z, cg_p0, cg_p1, cg_q, cg_t, cg_part_g, cg_part_r, cg_part_t, cg_qd;
     DBuf<CgState> cst;
     int cg_parity = 0;
     bool cg_ready = false;         // lsq_iterate state initialised (CG)

@@ -41,13 +41,14 @@ def _synthetic_system(name='t64', stiff=False):
     return S, fs, w, rhs
 
 
-@pytest.mark.parametrize('which', ['sf3d', 'nb_xt', 't64'])
+@pytest.mark.parametrize('which', ['sf3d', 'nb_xt', 't64', 't256'])
 def test_normal_operator_equals_assembled_normal_matrix(gpu_available, which):
     """q = N p from the class-coefficient stencil + Adᵀ(Ad p) equals Aᵀ(A p) computed with the
     formed A (bit-identical to the reference's matrix) on random p, every column incl. the
-    boundary classes; removed (reference-epoch) columns carry p = 0."""
-    if which == 't64':
-        S, fs, w, rhs = _synthetic_system()
+    boundary classes; removed (reference-epoch) columns carry p = 0.  t256 has dim-1 tiles clear
+    of both edges (the wave-uniform coefficient path); the small grids only edge tiles."""
+    if which in ('t64', 't256'):
+        S, fs, w, rhs = _synthetic_system(which)
     else:
         g, fs, w, rhs = _golden_system(which)
     rng = np.random.default_rng(7)

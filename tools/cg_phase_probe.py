@@ -1,6 +1,7 @@
-"""Development probe: per-phase cost of the CGNR normal-stencil kernel on a BASELINE config.
-LSQ_CG_DBG bits: 1 skip the stencil compute, 4 skip the staging loads, 8 skip the q stores,
-16 replace the stencil sum by the centre value.  Prints one JSON line per mode."""
+"""Development probe: per-kernel times of one CGNR iteration (block-Jacobi) on a BASELINE config.
+Tuning variables the library reads when it builds the normal-stencil description (e.g.
+LSQ_CG_RPW) are taken from the environment, so run one process per setting.
+Usage: python tools/cg_phase_probe.py [config]  — prints one JSON line."""
 import json
 import os
 import sys
@@ -10,8 +11,7 @@ import bench  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else 'c4'
 fs, rhs, w, setup = bench.build_system(cfg, 0)
-for mode in [int(a) for a in sys.argv[2:]] or (0, 1, 4, 5):
-    os.environ['LSQ_CG_DBG'] = str(mode)
-    p = fs.solver.profile_cg(reps=10, precond=3)
-    print(json.dumps({'mode': mode, **{k: v for k, v in p.items() if k != 'bytes'}}), flush=True)
+p = fs.solver.profile_cg(reps=10, precond=3)
+env = {k: v for k, v in os.environ.items() if k.startswith('LSQ_CG')}
+print(json.dumps({'config': cfg, 'env': env, **{k: v for k, v in p.items() if k != 'bytes'}}), flush=True)
 fs.close()
