@@ -253,7 +253,7 @@ struct System {
     DBuf<CgDesc> cgd;
     DBuf<double> cg_coef, cg_coefc;  // class-row tables: offset-major (tile mode), group × t (column mode)
     std::vector<double> cg_wkey;   // part row scales the table was built for
-    DBuf<double> cg_x, cg_s, cg_z, cg_p0, cg_p1, cg_q, cg_t, cg_part_g, cg_part_r, cg_part_t, cg_qd;
+    DBuf<double> cg_x, cg_s, cg_z, cg_p0, cg_p1, cg_q, cg_t, cg_part_g, cg_part_r, cg_part_t;
     DBuf<CgState> cst;
     int cg_parity = 0;
     bool cg_ready = false;         // lsq_iterate state initialised (CG)

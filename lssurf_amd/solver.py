@@ -171,8 +171,6 @@ class LSQSolver:
         self._check(self._L.lsq_profile_cg(self._h, int(reps), int(precond), ptr(o)), 'lsq_profile_cg')
         d = dict(zip(['cg_data', 'cg_normal', 'cg_update', 'cg_scalars'], o[:4].tolist()))
         d['bytes'] = {'cg_data': float(o[4]), 'cg_normal': float(o[5]), 'cg_update': float(o[6])}
-        if o[7] > 0:   # column mode: cg_normal includes the ATd·t launch, timed alone here
-            d['cg_atd'] = float(o[7])
         return d
 
     def normal_apply(self, p_full):
