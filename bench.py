@@ -110,8 +110,9 @@ def cpu_baseline(fs, b_weighted, sample_iters, threads):
 
 
 # kernel symbols per role: LSQR (assembled-SELL operator / structured stencil operator), CGNR
+# (a role's launches per iteration: its PMC bytes are the sum over the symbols found)
 KERNEL_SYMBOL = {0: {'xw_spmv': ('k_xw_spmv(', 'k_mf_fwd('), 'spmtv': ('k_spmtv(', 'k_mf_spmtv(')},
-                 1: {'cg_data': ('k_cg_data(',), 'cg_normal': ('k_cg_normal(',),
+                 1: {'cg_data': ('k_cg_data(', 'k_cg_atdq('), 'cg_normal': ('k_cg_normal(', 'k_cg_normal_col(', 'k_cg_xedge('),
                      'cg_update': ('k_cg_block(', 'k_cg_jacobi(')}}
 
 
@@ -145,15 +146,17 @@ def pmc_traffic(config, op, method=0, precond=1, timeout=300):
             if r.returncode != 0:
                 return None, f'rocprofv3 --pmc {ctr} rc={r.returncode}'
             files = [os.path.join(dp, f) for dp, _, fs in os.walk(out) for f in fs if f.endswith('counter_collection.csv')]
+            rows = [row for f in files for row in csv.DictReader(open(f)) if row['Counter_Name'] == ctr]
             for kernel, syms in KERNEL_SYMBOL[method].items():
-                xs = []
-                for f in files:
-                    for row in csv.DictReader(open(f)):
-                        if any(x in row['Kernel_Name'] for x in syms) and row['Counter_Name'] == ctr:
-                            xs.append(float(row['Counter_Value']))
-                if not xs:
+                tot, found = 0.0, False
+                for sym in syms:   # mean per launch of each symbol, summed over the role's symbols
+                    xs = [float(r['Counter_Value']) for r in rows if sym in r['Kernel_Name']]
+                    if xs:
+                        tot += sum(xs) / len(xs)
+                        found = True
+                if not found:
                     return None, f'no {ctr} samples for {kernel}'
-                vals[kernel, ctr] = sum(xs) / len(xs) * 1024.0
+                vals[kernel, ctr] = tot * 1024.0
     return {k: {'fetch_bytes': 2.0 * vals[k, 'FETCH_SIZE'], 'write_bytes': vals[k, 'WRITE_SIZE'],
                 'total': 2.0 * vals[k, 'FETCH_SIZE'] + vals[k, 'WRITE_SIZE']} for k in KERNEL_SYMBOL[method]}, None
 
