@@ -83,11 +83,21 @@ class _Dist:
         return self.ds.info()
 
     def iterate(self, rhs, iters, op=0, precond=1, method=0):
-        return self.ds.iterate(None, None, iters)
+        return self.ds.iterate(None, None, iters, precond=precond, method=method)
 
     def solve(self, rhs, op=0, precond=1, method=0):
-        x = self.ds.solve(None, None)
+        x = self.ds.solve(None, None, precond=precond, method=method)   # the single-GPU solve's tolerances
         return x, self.ds.stats
+
+    def profile_cg(self, reps=10, precond=3):
+        import ctypes
+        o = np.zeros(8)
+        rc = self.ds.L.lsq_profile_cg(self.ds.h, int(reps), int(precond), o.ctypes.data_as(ctypes.c_void_p))
+        if rc != 0:
+            raise RuntimeError('lsq_profile_cg: ' + self.ds.L.lsq_last_error(self.ds.h).decode())
+        d = dict(zip(['cg_data', 'cg_normal', 'cg_update', 'cg_scalars'], o[:4].tolist()))
+        d['bytes'] = {'cg_data': float(o[4]), 'cg_normal': float(o[5]), 'cg_update': float(o[6])}
+        return d
 
     def profile_kernels(self, reps=10, op=0):
         import ctypes
@@ -209,8 +219,8 @@ def main():
     if args.e2e:
         return e2e(args.config, args.e2e)
     world = int(os.environ.get('WORLD_SIZE', '1'))
-    if world > 1 or args.dist:   # distributed ranks run LSQR with column scaling
-        args.method, args.precond = 'lsqr', 1
+    if (world > 1 or args.dist) and args.method == 'lsqr':   # distributed LSQR: column scaling only
+        args.precond = 1
     meth = 1 if args.method == 'cgnr' else 0
     if args.pmc_child:
         return pmc_child(args.config, args.op, meth, args.precond)
@@ -290,7 +300,7 @@ def main():
         solve = {'solve_time_s': sst['time_s'], 'solve_iters': int(sst['iters']), 'solve_istop': int(sst['istop']),
                  'solve_method': ['lsqr', 'cgnr'][int(sst.get('method', 0))],
                  'solve_precond': {1: 'column scaling', 3: 'block-Jacobi per (y,x) node'}.get(args.precond, args.precond)}
-        if meth == 1:
+        if meth == 1 and not isinstance(solver, _Dist):   # distributed LSQR has no block-Jacobi
             xl, sl = solver.solve(rhs, op=args.op, precond=args.precond, method=0)
             solve['solve_lsqr'] = {'solve_time_s': sl['time_s'], 'solve_iters': int(sl['iters']),
                                    'solve_istop': int(sl['istop'])}

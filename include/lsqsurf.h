@@ -44,8 +44,9 @@ typedef struct lsq_handle lsq_handle;
 typedef struct lsq_opts {
     int32_t method;        /* 0 = LSQR (Paige & Saunders 1982); 1 = CGNR: preconditioned CG on  */
                            /*     the normal equations with the fused normal-stencil operator   */
-                           /*     (structured single-GPU systems, precond 1 or 3; other systems */
-                           /*     fall back to LSQR and report method 0 in lsq_stats)           */
+                           /*     (structured systems, single-GPU or structured ranks; precond  */
+                           /*     1 or 3; other single-GPU systems fall back to LSQR and report */
+                           /*     method 0 in lsq_stats)                                        */
     int32_t precond;       /* 0 = none, 1 = column (Jacobi) scaling, 2 = dense Cholesky R⁻¹   */
                            /*     (exact right preconditioner; n up to a few 10^4), 3 = block-  */
                            /*     Jacobi: R_b⁻¹ of every column block (lsq_set_column_blocks;   */
@@ -130,7 +131,9 @@ int lsq_set_row_mask(lsq_handle* h, const uint8_t* keep);
  * unlisted columns are singleton blocks.  For smooth_fit a block is one (y, x) node: its z0
  * column and its dz columns of every kept epoch.  The factors R_b (AᵀA restricted to the block
  * = R_bᵀR_b, with the current row weights / mask) are rebuilt on the device when weights change.
- * NULL / 0 blocks clears the structure (every column its own block). */
+ * NULL / 0 blocks clears the structure (every column its own block).  On a structured rank
+ * (lsq_dist_set_halo) the blocks are the rank's owned nodes in its local compact ids, factored
+ * from the rank's own rows; ghost columns stay outside every block. */
 int lsq_set_column_blocks(lsq_handle* h, int64_t n_blocks, const int64_t* block_ptr, const int32_t* cols);
 
 int lsq_shape(lsq_handle* h, int64_t* m, int64_t* n, int64_t* nnz);

@@ -175,7 +175,7 @@ int lsq_set_row_weight(lsq_handle* h, const double* row_weight) {
 int lsq_set_column_blocks(lsq_handle* h, int64_t n_blocks, const int64_t* block_ptr, const int32_t* cols) {
     return guarded(h, [&](lsq::System& S) {
         if (!S.G.rp.p) return fail(S, "lsq_set_column_blocks: no matrix");
-        if (S.dist) return fail(S, "lsq_set_column_blocks: single-GPU handles only");
+        if (S.dist && !S.dist_mf) return fail(S, "lsq_set_column_blocks: single-GPU or structured-rank handles only");
         lsq::graph_cache_drop(&S);
         lsq::set_column_blocks(S, n_blocks > 0 ? n_blocks : 0, block_ptr, cols);
         return 0;
@@ -259,7 +259,7 @@ int lsq_solve(lsq_handle* h, const double* b, double* x_inout, const lsq_opts* o
             lsq::Group G;
             G.ranks = {&S};
             double* xs[1] = {x_inout};
-            return lsq::group_solve(G, &b, xs, *o, s);
+            return o->method == 1 ? lsq::group_cg_solve(G, &b, xs, *o, s) : lsq::group_solve(G, &b, xs, *o, s);
         }
         if (o->method == 1 && lsq::cg_available(S, o->precond)) return lsq::cg_solve(S, b, x_inout, *o, s);
         if (s) s->method = 0;
@@ -277,7 +277,7 @@ int lsq_iterate(lsq_handle* h, const double* b, int64_t iters, const lsq_opts* o
             if (S.virt) return fail(S, "lsq_iterate: a virtual rank iterates through lsq_vgroup_iterate");
             lsq::Group G;
             G.ranks = {&S};
-            return lsq::group_iterate(G, &b, iters, *o, s);
+            return o->method == 1 ? lsq::group_cg_iterate(G, &b, iters, *o, s) : lsq::group_iterate(G, &b, iters, *o, s);
         }
         if (o->method == 1 && lsq::cg_available(S, o->precond)) return lsq::cg_iterate(S, b, iters, *o, s);
         if (s) s->method = 0;
@@ -607,7 +607,8 @@ int lsq_vgroup_solve(lsq_vgroup* g, const double* const* b, double* const* x, co
     return vguarded(g, [&](lsq::Group& G) {
         lsq_opts d;
         lsq_default_opts(&d);
-        return lsq::group_solve(G, b, x, o ? *o : d, s);
+        const lsq_opts& oo = o ? *o : d;
+        return oo.method == 1 ? lsq::group_cg_solve(G, b, x, oo, s) : lsq::group_solve(G, b, x, oo, s);
     });
 }
 
@@ -615,7 +616,8 @@ int lsq_vgroup_iterate(lsq_vgroup* g, const double* const* b, int64_t iters, con
     return vguarded(g, [&](lsq::Group& G) {
         lsq_opts d;
         lsq_default_opts(&d);
-        return lsq::group_iterate(G, b, iters, o ? *o : d, s);
+        const lsq_opts& oo = o ? *o : d;
+        return oo.method == 1 ? lsq::group_cg_iterate(G, b, iters, oo, s) : lsq::group_iterate(G, b, iters, oo, s);
     });
 }
 

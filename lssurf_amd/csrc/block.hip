@@ -174,20 +174,30 @@ void ensure_blocks(System& S) {
     if (S.nblk == 0) set_column_blocks(S, 0, nullptr, nullptr);
 }
 
-void block_factor(System& S) {
+// (AᵀA)_bb of every block into blk_Ri (packed upper), from the system's own rows
+void block_normal(System& S) {
     ensure_blocks(S);
     const int npk = S.blk_kmax * (S.blk_kmax + 1) / 2;
     if (S.blk_Ri.n != (int64_t)npk * S.nblk) S.blk_Ri.alloc((int64_t)npk * S.nblk);
-    DBuf<unsigned long long> nd(1);
-    nd.zero(S.stream);
     hipLaunchKernelGGL(k_block_normal, dim3(grid_for(S.nblk * npk)), dim3(BLOCK), 0, S.stream, S.nblk, S.blk_kmax,
                        S.blk_ptr.p, S.blk_cols.p, S.GT.rp.p, S.GT.ci.p, S.GT.val.p, S.rs.p, S.blk_Ri.p);
     KERNEL_CHECK();
+}
+
+// blk_Ri: (AᵀA)_bb -> R_b⁻¹ in place
+void block_factor_in_place(System& S) {
+    DBuf<unsigned long long> nd(1);
+    nd.zero(S.stream);
     hipLaunchKernelGGL(k_block_factor, dim3(grid_for(S.nblk)), dim3(BLOCK), 0, S.stream, S.nblk, S.blk_ptr.p,
                        S.blk_kmax, S.blk_Ri.p, nd.p);
     KERNEL_CHECK();
     HIP_CHECK(hipStreamSynchronize(S.stream));
     S.blk_valid = true;
+}
+
+void block_factor(System& S) {
+    block_normal(S);
+    block_factor_in_place(S);
 }
 
 }  // namespace lsq

@@ -929,4 +929,6 @@ void lsqr_get_rinv(System& S, double* h_Ri) {
 
 #include "lsqr_dist.inc"
 
+#include "lsqr_cg_dist.inc"
+
 }  // namespace lsq

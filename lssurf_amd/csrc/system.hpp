@@ -215,6 +215,7 @@ struct System {
     DBuf<int32_t> blk_cols;         // compact ids
     DBuf<int32_t> blk_full;         // full ids (stencil operator v-space)
     DBuf<double> blk_Ri;
+    DBuf<double> blk_tmp;           // structured ranks: block partial sums by column (kmax × n_full) for the halo
     bool blk_valid = false;
 
     // dense factor (precond 2 / error propagation): R and R⁻¹, npad x npad row-major
@@ -285,6 +286,8 @@ struct Group {
 void group_prepare_virtual(Group& G);
 int group_solve(Group& G, const double* const* h_b, double* const* h_x, const lsq_opts& o, lsq_stats* stats);
 int group_iterate(Group& G, const double* const* h_b, int64_t iters, const lsq_opts& o, lsq_stats* stats);
+int group_cg_solve(Group& G, const double* const* h_b, double* const* h_x, const lsq_opts& o, lsq_stats* stats);
+int group_cg_iterate(Group& G, const double* const* h_b, int64_t iters, const lsq_opts& o, lsq_stats* stats);
 void referenced_cols(System& S, uint8_t* h_flags);
 void relabel_columns(System& S, const int32_t* h_map, int64_t n_local);
 
@@ -306,6 +309,8 @@ void csr_spmv_rows(System& S, int64_t first, int64_t count, const double* dx, do
 void set_column_blocks(System& S, int64_t nb, const int64_t* ptr, const int32_t* cols);
 void ensure_blocks(System& S);                     // default structure if none was set
 void block_factor(System& S);                      // R_b⁻¹ for the current row scale
+void block_normal(System& S);                      // (AᵀA)_bb of the system's own rows into blk_Ri
+void block_factor_in_place(System& S);             // blk_Ri: (AᵀA)_bb -> R_b⁻¹
 
 // dense.hip
 void dense_factor(System& S);                     // R, R⁻¹ of diag(rs)·G (throws if not SPD)

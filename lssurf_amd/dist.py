@@ -205,6 +205,43 @@ def _install_halo(L, h, prob, halo):
                             ptr(send_idx), ptr(recv_cnt), ptr(recv_idx)), 'lsq_dist_set_halo')
 
 
+def window_node_blocks(prob, keep_cols):
+    """Block-Jacobi blocks (precond 3) of a rank: the node blocks of constraint_functions.
+    node_column_blocks for every node of the rank's window (owned and ghost), in the rank's local
+    compact column ids (block_ptr, cols), or None when the grids have no node-block structure.
+    The ghost blocks carry the rank's partial (AᵀA)_bb to their owners (group_block_factor); the
+    update kernels skip ghost columns."""
+    from .constraint_functions import node_column_blocks
+    grids = {}
+    for g in prob['grid_objs']:
+        grids['dz' if g.N_dims == 3 else 'z0'] = g
+    blocks = node_column_blocks(grids, keep_cols)
+    if blocks is None:
+        return None
+    bptr, bcols = blocks
+    keep_cols = np.asarray(keep_cols)
+    l2g = prob['l2g']
+    gfull = keep_cols[bcols]
+    lf = np.minimum(np.searchsorted(l2g, gfull), l2g.size - 1)
+    ok = l2g[lf] == gfull
+    keep_local = np.asarray(prob['keep'])
+    lc = np.minimum(np.searchsorted(keep_local, lf), keep_local.size - 1)
+    ok &= keep_local[lc] == lf
+    lens = np.diff(bptr)
+    blk_ok = np.add.reduceat(ok.astype(np.int64), bptr[:-1]) == lens   # every column in the window and kept
+    sel = np.repeat(blk_ok, lens)
+    return np.r_[0, np.cumsum(lens[blk_ok])].astype(np.int64), lc[sel].astype(np.int32)
+
+
+def _install_blocks(L, h, prob, keep_cols):
+    blocks = window_node_blocks(prob, keep_cols)
+    if blocks is None:
+        return False
+    bptr, bcols = blocks
+    _HandleView(L, h).check(L.lsq_set_column_blocks(h, bptr.size - 1, ptr(bptr), ptr(bcols)), 'lsq_set_column_blocks')
+    return True
+
+
 def window_owned_solution(prob, x_local, x_out):
     """Scatter the owned columns of a rank's local compact solution into the global compact x."""
     full = prob['keep']
@@ -348,6 +385,7 @@ class DistFitSystem(_Base):
             _form_window(self.L, self.h, self.prob)
             _install_halo(self.L, self.h, self.prob,
                           window_halo(self.prob['grid_objs'], self.partition, rank, self.prob['halo']))
+            self.has_blocks = _install_blocks(self.L, self.h, self.prob, keep_cols)
             self.n_x = self.prob['keep'].size
         else:            # owned rows, relabelled compact columns, assembled SELL operator
             self.prob = rank_problem(G_data, Gc, self.partition, rank)
@@ -362,6 +400,7 @@ class DistFitSystem(_Base):
             _install_layout(self.L, self.h, self.layout, self.plan)
             self.owned_cols = self.layout[4]
             self.n_x = self.layout[2]
+            self.has_blocks = False
         self.stats = None
 
     def scatter_owned(self, x_local, x_out):
@@ -383,19 +422,20 @@ class DistFitSystem(_Base):
         wl = as_c(np.asarray(w)[self.prob['rows']], np.float64)
         _HandleView(self.L, self.h).check(self.L.lsq_set_row_weight(self.h, ptr(wl)), 'lsq_set_row_weight')
 
-    def solve(self, row_weight, rhs, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1):
+    def solve(self, row_weight, rhs, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, method=0):
+        """method 0: LSQR (precond 0/1); 1: CGNR (precond 1 Jacobi, 3 block-Jacobi; structured ranks)."""
         b = self._b(row_weight, rhs)
         x = np.zeros(self.n_x)
-        o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond))
+        o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond), method=int(method))
         st = LsqStats()
         _HandleView(self.L, self.h).check(self.L.lsq_solve(self.h, ptr(b), ptr(x), ctypes.byref(o), ctypes.byref(st)),
                                           'lsq_solve')
         self.stats = st.as_dict()
         return x   # this rank's columns: scatter_owned() places them in the global vector
 
-    def iterate(self, row_weight, rhs, iters, precond=1):
+    def iterate(self, row_weight, rhs, iters, precond=1, method=0):
         b = self._b(row_weight, rhs)
-        o = default_opts(precond=int(precond))
+        o = default_opts(precond=int(precond), method=int(method))
         st = LsqStats()
         _HandleView(self.L, self.h).check(
             self.L.lsq_iterate(self.h, ptr(b), int(iters), ctypes.byref(o), ctypes.byref(st)), 'lsq_iterate')
@@ -431,6 +471,7 @@ class VirtualDistFitSystem(_Base):
                 prob = window_problem(G_data, Gc, self.partition, r, keep_cols)
                 _form_window(self.L, h, prob)
                 _install_halo(self.L, h, prob, window_halo(prob['grid_objs'], self.partition, r, prob['halo']))
+                _install_blocks(self.L, h, prob, keep_cols)
                 self.probs.append(prob)
             self.nx = [p['keep'].size for p in self.probs]
         else:
@@ -463,12 +504,12 @@ class VirtualDistFitSystem(_Base):
             self._b_local = [as_c(np.asarray(rhs)[prob['rows']], np.float64) for prob in self.probs]
         return self._b_local
 
-    def solve(self, row_weight, rhs, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1):
+    def solve(self, row_weight, rhs, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, method=0):
         bs = self._bs(row_weight, rhs)
         xs = [np.zeros(k) for k in self.nx]
         bp = (ctypes.c_void_p * self.nranks)(*[b.ctypes.data for b in bs])
         xp = (ctypes.c_void_p * self.nranks)(*[x.ctypes.data for x in xs])
-        o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond))
+        o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond), method=int(method))
         st = LsqStats()
         self._check(self.L.lsq_vgroup_solve(self.g, bp, xp, ctypes.byref(o), ctypes.byref(st)), 'lsq_vgroup_solve')
         self.stats = st.as_dict()
@@ -480,10 +521,10 @@ class VirtualDistFitSystem(_Base):
                 x[self.layouts[r][4]] = xr
         return x   # compact columns (same space as LSQSolver.solve)
 
-    def iterate(self, row_weight, rhs, iters, precond=1):
+    def iterate(self, row_weight, rhs, iters, precond=1, method=0):
         bs = self._bs(row_weight, rhs)
         bp = (ctypes.c_void_p * self.nranks)(*[b.ctypes.data for b in bs])
-        o = default_opts(precond=int(precond))
+        o = default_opts(precond=int(precond), method=int(method))
         st = LsqStats()
         self._check(self.L.lsq_vgroup_iterate(self.g, bp, int(iters), ctypes.byref(o), ctypes.byref(st)),
                     'lsq_vgroup_iterate')

@@ -120,3 +120,68 @@ def test_rccl_one_rank(gpu_available, structured):
     ds.scatter_owned(xo, x)
     assert std['istop'] in (1, 2)
     assert np.linalg.norm(x - x1) / np.linalg.norm(x1) <= 1e-8
+
+
+# ---- CGNR over ranks (lsqr_cg_dist.inc) -------------------------------------------------------
+def _single_cg(S, keep, w, rhs, precond):
+    fs = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, grids=S['grids'])
+    x = fs.solve(w, np.ones(fs.n_data, bool), rhs, atol=1e-12, btol=1e-12, conlim=1e12, precond=precond, method=1)
+    st = fs.stats
+    fs.close()
+    return x, st
+
+
+@pytest.mark.parametrize('precond', [3, 1])
+@pytest.mark.parametrize('nranks', [2, 3, 4])
+def test_virtual_ranks_cgnr_match_single_gpu(gpu_available, nranks, precond):
+    """Distributed CGNR (normal-stencil ranks, reverse halo of q, forward halo of z) runs the
+    single-GPU recurrence with the same preconditioner (Jacobi from the global column norms;
+    block-Jacobi from the node blocks summed over the ranks), so the iteration counts agree and
+    the solutions match to the solver tolerance."""
+    S, kw = _t64()
+    keep, w, rhs = _problem(S, kw)
+    x1, st1 = _single_cg(S, keep, w, rhs, precond)
+    assert st1['method'] == 1
+    vd = dist.VirtualDistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, nranks)
+    try:
+        xd = vd.solve(w, rhs, atol=1e-12, btol=1e-12, conlim=1e12, precond=precond, method=1)
+        std = vd.stats
+    finally:
+        vd.close()
+    assert std['method'] == 1 and std['istop'] in (1, 2), std
+    slack = 3
+    assert abs(std['iters'] - st1['iters']) <= slack, (std['iters'], st1['iters'])
+    assert np.linalg.norm(xd - x1) / np.linalg.norm(x1) <= 1e-8
+
+
+@pytest.mark.parametrize('precond', [3, 1])
+def test_virtual_ranks_cgnr_golden_exact_solution(gpu_available, precond):
+    g = golden('sys_sf3d.npz')
+    kw = golden_kwargs(g)
+    S = LS.smooth_fit(data=golden_points(g), return_fit_objects=True, **kw)
+    keep, w, rhs = _problem(S, kw)
+    vd = dist.VirtualDistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, 2)
+    try:
+        x = vd.solve(w, rhs, atol=1e-12, btol=1e-12, conlim=1e12, maxit=200000, precond=precond, method=1)
+    finally:
+        vd.close()
+    xs = g['x']
+    assert np.linalg.norm(x - xs) / np.linalg.norm(xs) <= 1e-6
+    assert np.max(np.abs(x - xs)) <= 1e-4
+
+
+def test_virtual_ranks_cgnr_iterate_matches_solve_prefix(gpu_available):
+    """lsq_iterate (fixed iteration count, the bench path) on ranks runs the same iterations as the
+    solve: after k iterations the residual estimate equals the solve's after k."""
+    S, kw = _t64()
+    keep, w, rhs = _problem(S, kw)
+    vd = dist.VirtualDistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, 2)
+    try:
+        st = vd.iterate(w, rhs, 20, precond=3, method=1)
+        x = vd.solve(None, None, atol=1e-12, btol=1e-12, conlim=1e12, maxit=20, precond=3, method=1)
+        st2 = vd.stats
+    finally:
+        vd.close()
+    assert st['method'] == 1 and st['iters'] == 20 and st2['iters'] == 20
+    assert np.isclose(st['r1norm'], st2['r1norm'], rtol=1e-10)
+    assert np.all(np.isfinite(x))

@@ -29,7 +29,7 @@ def _problem():
     return S, keep, w, rhs
 
 
-def _rank(rank, world, port, structured, outq):
+def _rank(rank, world, port, structured, outq, opts=TOL):
     os.environ['NCCL_HOSTID'] = f'lsq-test-host-{rank}'
     os.environ.setdefault('NCCL_SOCKET_IFNAME', 'lo')
     os.environ.setdefault('NCCL_IB_DISABLE', '1')
@@ -41,7 +41,7 @@ def _rank(rank, world, port, structured, outq):
         ds = dist.DistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, rank, world, device=0,
                                 structured=structured)
         try:
-            xl = ds.solve(w, rhs, **TOL)
+            xl = ds.solve(w, rhs, **opts)
             st = ds.stats
         finally:
             ds.close()
@@ -54,13 +54,19 @@ def _rank(rank, world, port, structured, outq):
         tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize('structured', [True, False])
-def test_two_rccl_ranks_match_single_gpu(gpu_available, structured):
+CG_TOL = dict(atol=1e-12, btol=1e-12, conlim=1e12, precond=3, method=1)
+
+
+@pytest.mark.parametrize('structured,opts', [(True, TOL), (False, TOL), (True, CG_TOL)],
+                         ids=['lsqr-structured', 'lsqr-assembled', 'cgnr-blockjacobi'])
+def test_two_rccl_ranks_match_single_gpu(gpu_available, structured, opts):
+    """cgnr-blockjacobi: CGNR + block-Jacobi over RCCL (halos of q and z, two all-reduces per
+    iteration, node blocks summed over the ranks before factoring)."""
     import torch.multiprocessing as mp
     from lssurf_amd.smooth_fit import FitSystem
     S, keep, w, rhs = _problem()
-    fs = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N)
-    x1 = fs.solve(w, np.ones(fs.n_data, bool), rhs, **TOL)
+    fs = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, grids=S['grids'])
+    x1 = fs.solve(w, np.ones(fs.n_data, bool), rhs, **opts)
     it1 = fs.stats['iters']
     fs.close()
     with socket.socket() as s:
@@ -68,7 +74,7 @@ def test_two_rccl_ranks_match_single_gpu(gpu_available, structured):
         port = s.getsockname()[1]
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    procs = [ctx.Process(target=_rank, args=(r, 2, port, structured, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, structured, q, opts)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=400) for _ in procs]
