@@ -35,6 +35,13 @@ def build_system(config, device):
     from lssurf_amd.constraint_functions import reference_epoch_keep_cols
     from lssurf_amd.smooth_fit import FitSystem
     t0 = time.time()
+    if config in synthetic.CONFIGS_2D:   # 2-D z0-only lin_op system (BASELINE C2), structured formation
+        G, Gc, grid, w, rhs = synthetic.system2d(config)
+        t1 = time.time()
+        fs = FitSystem(G, Gc, np.arange(G.col_N), G.col_N, device=device, grids={'z0': grid})
+        fs.solver.set_row_weight(w)
+        fs.solver.set_row_mask(np.ones(w.size, bool))
+        return fs, rhs, w, {'host_assembly_s': t1 - t0, 'device_formation_s': time.time() - t1}
     D, kw = synthetic.points(config)
     S = LS.smooth_fit(data=D, return_fit_objects=True, VERBOSE=False, **kw)
     keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch'])
@@ -221,6 +228,10 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     if (world > 1 or args.dist) and args.method == 'lsqr':   # distributed LSQR: column scaling only
         args.precond = 1
+    if args.config in __import__('lssurf_amd.synthetic', fromlist=['x']).CONFIGS_2D:
+        if world > 1 or args.dist:
+            raise SystemExit('bench: the 2-D configs run on one GPU')
+        args.precond = 1   # no node blocks in a z0-only system: Jacobi
     meth = 1 if args.method == 'cgnr' else 0
     if args.pmc_child:
         return pmc_child(args.config, args.op, meth, args.precond)
@@ -323,7 +334,8 @@ def main():
             'ms_per_step': ms_per_step, 'higher_is_better': True,
             'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f64',
             'data': 'synthetic (SURVEY.md §8(d) point cloud)',
-            'config': {'workload': f'smooth_fit LSQR, {args.config}', 'rank0_system': info, 'rows': gm, 'cols': gn,
+            'config': {'workload': f'{"2-D lin_op (z0 only)" if args.config in ("c2", "t2d") else "smooth_fit"} solve, {args.config}',
+                       'rank0_system': info, 'rows': gm, 'cols': gn,
                        'nnz': gZ, 'precond': {1: 'column scaling', 3: 'block-Jacobi per (y,x) node'}.get(args.precond, args.precond),
                        'operator': 'structured stencil rows + SELL data rows'
                        if (fs.structured if isinstance(solver, _Dist) else info.get('stencil_op') and args.op == 0)

@@ -44,3 +44,39 @@ def points(name, config_id=None):
         + 0.5 * t * np.exp(-((x - ctr['x']) ** 2 + (y - ctr['y']) ** 2) / (W['x'] / 4) ** 2) \
         + rng.normal(0, 0.1, npts)
     return pc.data().from_dict({'x': x, 'y': y, 'time': t, 'z': z, 'sigma': np.full(npts, 0.1)}), kw
+
+
+# 2-D z0-only configurations (BASELINE config C2: notebooks/smooth_fit_demo_aniso.ipynb style —
+# interp + grad2_z0 + grad_z0 formed with lin_op and handed to the solver directly):
+# id: (nodes per side, points)
+CONFIGS_2D = {
+    'c2': (1024, 500_000),
+    't2d': (64, 4_000),
+}
+E_RMS_2D = {'d2z0_dx2': 0.03, 'dz0_dx': 75.}
+
+
+def system2d(name):
+    """(G_data, Gc, grid, row_weight, rhs) of a 2-D config: domain (n−1)·100 m square from 0,
+    spacing 100 m, points uniform from default_rng(20251121 + 100 + index), z = 10 sin(2πx/L)
+    cos(2πy/L') + N(0, 0.1), σ = 0.1; constraint σ = E_RMS / sqrt(cell area) as in
+    constraint_functions (the structure of tests/golden sys_lin2d)."""
+    from .fd_grid import fd_grid
+    from .lin_op import lin_op
+    n, npts = CONFIGS_2D[name]
+    rng = np.random.default_rng(20251121 + 100 + list(CONFIGS_2D).index(name))
+    W = (n - 1) * 100.
+    g = fd_grid([[0., W], [0., W]], [100., 100.], name='z0')
+    y, x = rng.uniform(0, W, npts), rng.uniform(0, W, npts)
+    z = 10 * np.sin(2 * np.pi * x / (W / 2)) * np.cos(2 * np.pi * y / (W / 3)) + rng.normal(0, 0.1, npts)
+    sigma = np.full(npts, 0.1)
+    G = lin_op(g, name='interp_z').interp_mtx([y, x])
+    root = np.sqrt(np.prod(g.delta))
+    g2 = lin_op(g, name='grad2_z0').grad2(DOF='z0')
+    g2.expected = E_RMS_2D['d2z0_dx2'] / root * np.ones(g2.N_eq)
+    g1 = lin_op(g, name='grad_z0').grad(DOF='z0')
+    g1.expected = E_RMS_2D['dz0_dx'] / root * np.ones(g1.N_eq)
+    Gc = lin_op(None, name='constraints').vstack([g2, g1])
+    E_all = np.concatenate([sigma, g2.expected, g1.expected])
+    rhs = np.concatenate([z, np.zeros(Gc.N_eq)])
+    return G, Gc, g, 1. / E_all, rhs

@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 import lssurf_amd as LS
-from conftest import SYSTEMS, golden, golden_kwargs, golden_points
+from conftest import SYSTEMS, golden, golden_csr, golden_kwargs, golden_points
 from lssurf_amd.constraint_functions import reference_epoch_keep_cols
 from lssurf_amd.smooth_fit import FitSystem
 
@@ -171,3 +171,52 @@ def test_smooth_fit_cgnr_default(gpu_available):
         ok = np.isfinite(ref)
         assert np.linalg.norm(got[ok] - ref[ok]) / np.linalg.norm(ref[ok]) < 1e-6
     assert np.nanmax(np.abs(out['m']['dz'].dz - g['dz'])) < ABS
+
+
+def _lin2d_structured(g):
+    """tests/golden sys_lin2d (the notebook's 2-D z0-only system, C2's structure) rebuilt with
+    lssurf_amd.lin_op from the golden inputs and formed as a STRUCTURED system (lazy lin_op parts)."""
+    from lssurf_amd.fd_grid import fd_grid
+    from lssurf_amd.lin_op import lin_op
+    grid = fd_grid([[0., 2300.], [0., 2300.]], [100., 100.], name='z0')
+    G = lin_op(grid, name='interp_z').interp_mtx([g['in_y'], g['in_x']])
+    root = np.sqrt(np.prod(grid.delta))
+    g2 = lin_op(grid, name='grad2_z0').grad2(DOF='z0')
+    g2.expected = 0.03 / root * np.ones(g2.N_eq)
+    g1 = lin_op(grid, name='grad_z0').grad(DOF='z0')
+    g1.expected = 75. / root * np.ones(g1.N_eq)
+    Gc = lin_op(None, name='constraints').vstack([g2, g1])
+    w = 1. / np.concatenate([g['in_sigma'], g2.expected, g1.expected])
+    rhs = np.concatenate([g['in_z'], np.zeros(Gc.N_eq)])
+    fs = FitSystem(G, Gc, np.arange(G.col_N), G.col_N, grids={'z0': grid})
+    return fs, w, rhs
+
+
+def test_cgnr_2d_lin_op_system_exact_solution(gpu_available):
+    """C2 structure (2-D z0 grid, 1 node along dim 2: the MAXT = 1 column kernel): the lin_op
+    system forms as a structured system, its normal operator equals the formed AᵀA, and CGNR
+    (Jacobi) reaches the golden exact solution."""
+    g = golden('sys_lin2d.npz')
+    fs, w, rhs = _lin2d_structured(g)
+    try:
+        assert fs.formation == 'stencil'
+        fs.solver.set_row_weight(w)
+        fs.solver.set_row_mask(np.ones(w.size, bool))
+        ok, why = fs.solver.cg_available(1)
+        assert ok, why
+        A = fs.solver.get_csr()
+        Ag = golden_csr(g)
+        assert abs(A - Ag).max() <= 1e-12 * abs(Ag).max()
+        rng = np.random.default_rng(3)
+        p = rng.standard_normal(A.shape[1])
+        q = fs.solver.normal_apply(p)
+        qr = A.T @ (A @ p)
+        assert np.abs(q - qr).max() <= 1e-12 * np.abs(qr).max()
+        x = fs.solve(w, np.ones(fs.n_data, bool), rhs, precond=1, method=1, maxit=200000, **TOL)
+        st = fs.stats
+    finally:
+        fs.close()
+    assert st['method'] == 1 and st['istop'] in (1, 2), st
+    xs = g['x']
+    assert np.linalg.norm(x - xs) / np.linalg.norm(xs) <= REL
+    assert np.max(np.abs(x - xs)) <= ABS
