@@ -181,6 +181,22 @@ void set_column_blocks(System& S, int64_t nb, const int64_t* ptr, const int32_t*
     hipLaunchKernelGGL(k_full_ids, dim3(grid_for((int64_t)C.size())), dim3(BLOCK), 0, S.stream, (int64_t)C.size(),
                        S.blk_cols.p, S.mf ? S.keep.p : nullptr, S.blk_full.p);
     KERNEL_CHECK();
+    // affine column ids (every block the same size, column j of block b at base_j + b·stride_j)
+    S.blk_affine = false;
+    if (S.nblk > 1 && (int64_t)C.size() == S.nblk * kmax) {
+        std::vector<int32_t> F(C.size());
+        S.blk_full.download(F.data(), (int64_t)C.size(), S.stream);
+        HIP_CHECK(hipStreamSynchronize(S.stream));
+        bool ok = true;
+        for (int j = 0; j < kmax; ++j) {
+            S.blk_aff.base[j] = F[j];
+            S.blk_aff.stride[j] = (int64_t)F[kmax + j] - F[j];
+        }
+        for (int64_t b = 0; b < S.nblk && ok; ++b)
+            for (int j = 0; j < kmax; ++j)
+                ok = ok && (int64_t)F[b * kmax + j] == S.blk_aff.base[j] + b * S.blk_aff.stride[j];
+        S.blk_affine = ok;
+    }
     S.blk_Ri = DBuf<double>();
     S.blk_valid = false;
     S.blk_user = nb > 0;

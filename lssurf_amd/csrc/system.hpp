@@ -155,6 +155,9 @@ struct CgGrid {
     int32_t gl[CG_MAX_GRP];                  // in-row LDS offset dx·tpad of group g
     int32_t gc[CG_MAX_GRP];                  // offset of group g's MAXT × (2·DT_g + 1) coefficients in a row
 };
+struct BlkAffine {
+    int64_t base[16], stride[16];
+};
 struct CgDesc {
     int32_t n_grids, ntiles, lds_max, colmode;
     int32_t nedge, pad[3];                   // column mode: workgroups of k_cg_xedge
@@ -210,6 +213,10 @@ struct System {
     // lanes that apply it read it coalesced)
     int64_t nblk = 0;
     int blk_kmax = 0;
+    // every block has blk_kmax columns and column j of block b is full id base[j] + b·stride[j]
+    // (smooth_fit's node blocks): the CG update computes the ids instead of loading them
+    bool blk_affine = false;
+    BlkAffine blk_aff{};
     bool blk_user = false;          // blocks came from lsq_set_column_blocks
     DBuf<int64_t> blk_ptr;
     DBuf<int32_t> blk_cols;         // compact ids
