@@ -155,3 +155,29 @@ def test_windows_partition_rows_and_columns(nranks):
             theirs_recv = probs[q]['l2g'][pq[4][np.r_[0, np.cumsum(pq[3])][kk]:np.r_[0, np.cumsum(pq[3])][kk + 1]]]
             np.testing.assert_array_equal(mine_sent, theirs_recv)
             assert np.all(np.diff(mine_sent) > 0)
+
+
+@pytest.mark.parametrize('nranks', [2, 3])
+def test_window_node_blocks_cover_window_in_global_order(nranks):
+    """Block-Jacobi blocks of a rank (dist.window_node_blocks): one block per window node
+    (owned and ghost), in local compact ids whose global columns are exactly the single-GPU node
+    block of that node — same columns in the same order on every rank holding the node, which
+    is what lets group_block_factor sum the partial (AᵀA)_bb column by column."""
+    from lssurf_amd.constraint_functions import node_column_blocks
+    S, keep = _system()
+    part = dist.SlabPartition(S['grids']['dz'], nranks)
+    gptr, gcols = node_column_blocks(S['grids'], keep)
+    gblocks = {tuple(keep[gcols[gptr[b]:gptr[b + 1]]]) for b in range(gptr.size - 1)}
+    seen = {}
+    for r in range(nranks):
+        prob = dist.window_problem(S['G_data'], S['Gc'], part, r, keep)
+        bptr, bcols = dist.window_node_blocks(prob, keep)
+        assert bptr[0] == 0 and np.all(np.diff(bptr) > 0) and bcols.max() < prob['keep'].size
+        glob = prob['l2g'][prob['keep'][bcols]]                # local compact -> global full ids
+        for b in range(bptr.size - 1):
+            blk = tuple(glob[bptr[b]:bptr[b + 1]])
+            assert blk in gblocks
+            seen.setdefault(blk, set()).add(r)
+        assert np.unique(bcols).size == bcols.size            # a column in at most one block
+    assert set(seen) == gblocks                               # every node block lives on some rank
+    assert any(len(v) > 1 for v in seen.values())             # halo nodes are shared
