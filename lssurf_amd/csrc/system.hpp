@@ -160,7 +160,7 @@ struct BlkAffine {
 };
 struct CgDesc {
     int32_t n_grids, ntiles, lds_max, colmode;
-    int32_t nedge, pad[3];                   // column mode: workgroups of k_cg_xedge
+    int32_t nedge, maxt3, pad[2];            // column mode: workgroups of k_cg_xedge; 3-D column length
     CgGrid g[MF_MAX_GRIDS];
 };
 // PCG-on-AᵀA scalar state (device resident).  Quantities are those of CGLS on A·M^{-1/2}; the
