@@ -135,7 +135,7 @@ constexpr int CG_MAXI = 16;                 // (row, dim-2) items per wave of on
 // workgroup streams a strip of ty rows through an LDS ring (lsqr_cg.inc, cg_strip).
 constexpr int CG_MAXT = 16;
 constexpr int CG_MAX_GRP = 49;
-constexpr int CG_NCOL = 4;                  // ring staging: row-image columns per thread (row image ≤ CG_NCOL·256)
+constexpr int CG_NCW = 16;                  // ring staging: row-image columns per lane (a wave stages whole rows: ≤ 1024)
 struct CgGrid {
     int32_t shape[3], col0, node0;
     int32_t ty, nty, ntx, tile0;             // tiles of the grid: ids [tile0, tile0 + nty·ntx)
