@@ -129,8 +129,9 @@ def cpu_baseline(fs, b_weighted, sample_iters, threads):
 # kernel symbols per role: LSQR (assembled-SELL operator / structured stencil operator), CGNR
 # (a role's launches per iteration: its PMC bytes are the sum over the symbols found)
 KERNEL_SYMBOL = {0: {'xw_spmv': ('k_xw_spmv(', 'k_mf_fwd('), 'spmtv': ('k_spmtv(', 'k_mf_spmtv(')},
-                 1: {'cg_data': ('k_cg_data(', 'k_cg_atdq('), 'cg_normal': ('k_cg_normal(', 'k_cg_normal_col(', 'k_cg_xedge('),
-                     'cg_update': ('k_cg_block(', 'k_cg_jacobi(')}}
+                 1: {'cg_data': ('k_cg_data(', 'k_cg_atdq('),
+                     'cg_normal': ('k_cg_normal(', 'k_cg_normal_col<', 'k_cg_xedge('),
+                     'cg_update': ('k_cg_block<', 'k_cg_jacobi(')}}
 
 
 def pmc_traffic(config, op, method=0, precond=1, timeout=300):
