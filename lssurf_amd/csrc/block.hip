@@ -117,21 +117,15 @@ __global__ __launch_bounds__(BLOCK) void k_block_factor(int64_t nb, const int64_
     }
 }
 
-// M_b⁻¹ = R_b⁻¹ R_b⁻ᵀ (packed upper, as R_b⁻¹) for CG's z = M⁻¹ s: one thread per block
-__global__ __launch_bounds__(BLOCK) void k_block_minv(int64_t nb, const int64_t* __restrict__ ptr, int kmax,
-                                                      const double* __restrict__ Ri, double* __restrict__ Mi) {
-    const int npk = kmax * (kmax + 1) / 2;
-    for (int64_t b = (int64_t)blockIdx.x * BLOCK + threadIdx.x; b < nb; b += (int64_t)gridDim.x * BLOCK) {
-        const int k = (int)(ptr[b + 1] - ptr[b]);
-        double X[KB_PACK];
-        for (int e = 0; e < k * (k + 1) / 2; ++e) X[e] = Ri[b * npk + e];
-        for (int j = 0; j < k; ++j)
-            for (int i = 0; i <= j; ++i) {
-                double s = 0.0;   // Σ_{l ≥ j} X_il X_jl  (X upper: X_il = 0 for l < i)
-                for (int l = j; l < k; ++l) s += X[pk(i, l)] * X[pk(j, l)];
-                Mi[b * npk + pk(i, j)] = s;
-            }
-        for (int e = k * (k + 1) / 2; e < npk; ++e) Mi[b * npk + e] = 0.0;
+// R_b⁻¹ rounded to fp32 for CG's z = R_b⁻¹(R_b⁻ᵀ s): packed upper, block stride npks (npk rounded
+// up to even, so a run of blocks starts 8-byte aligned).  L L^T with a triangular L whose diagonal
+// is non-zero stays SPD whatever the rounding, so CG keeps a valid preconditioner at half the bytes.
+__global__ __launch_bounds__(BLOCK) void k_block_rinv32(int64_t nb, int npk, int npks, const double* __restrict__ Ri,
+                                                        float* __restrict__ Lf) {
+    for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < nb * npks; q += (int64_t)gridDim.x * BLOCK) {
+        const int64_t b = q / npks;
+        const int e = (int)(q - b * npks);
+        Lf[q] = e < npk ? (float)Ri[b * npk + e] : 0.0f;
     }
 }
 
@@ -225,10 +219,10 @@ void block_factor_in_place(System& S) {
     hipLaunchKernelGGL(k_block_factor, dim3(grid_for(S.nblk)), dim3(BLOCK), 0, S.stream, S.nblk, S.blk_ptr.p,
                        S.blk_kmax, S.blk_Ri.p, nd.p);
     KERNEL_CHECK();
-    const int npk = S.blk_kmax * (S.blk_kmax + 1) / 2;   // CGNR applies M_b⁻¹ = R_b⁻¹R_b⁻ᵀ in one product
-    if (S.blk_Mi.n != (int64_t)npk * S.nblk) S.blk_Mi.alloc((int64_t)npk * S.nblk);
-    hipLaunchKernelGGL(k_block_minv, dim3(grid_for(S.nblk)), dim3(BLOCK), 0, S.stream, S.nblk, S.blk_ptr.p, S.blk_kmax,
-                       S.blk_Ri.p, S.blk_Mi.p);
+    const int npk = S.blk_kmax * (S.blk_kmax + 1) / 2, npks = (npk + 1) & ~1;   // CGNR's fp32 copy
+    if (S.blk_Lf.n != (int64_t)npks * S.nblk) S.blk_Lf.alloc((int64_t)npks * S.nblk);
+    hipLaunchKernelGGL(k_block_rinv32, dim3(grid_for(S.nblk * npks)), dim3(BLOCK), 0, S.stream, S.nblk, npk, npks,
+                       S.blk_Ri.p, S.blk_Lf.p);
     KERNEL_CHECK();
     HIP_CHECK(hipStreamSynchronize(S.stream));
     S.blk_valid = true;

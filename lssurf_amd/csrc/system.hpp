@@ -222,7 +222,7 @@ struct System {
     DBuf<int32_t> blk_cols;         // compact ids
     DBuf<int32_t> blk_full;         // full ids (stencil operator v-space)
     DBuf<double> blk_Ri;
-    DBuf<double> blk_Mi;            // M_b⁻¹ = R_b⁻¹R_b⁻ᵀ (packed upper, same layout) for CGNR
+    DBuf<float> blk_Lf;             // R_b⁻¹ in fp32 for CGNR (packed upper, block stride npk rounded to even)
     DBuf<double> blk_tmp;           // structured ranks: block partial sums by column (kmax × n_full) for the halo
     bool blk_valid = false;
 
