@@ -104,6 +104,7 @@ class _Dist:
             raise RuntimeError('lsq_profile_cg: ' + self.ds.L.lsq_last_error(self.ds.h).decode())
         d = dict(zip(['cg_data', 'cg_normal', 'cg_update', 'cg_scalars'], o[:4].tolist()))
         d['bytes'] = {'cg_data': float(o[4]), 'cg_normal': float(o[5]), 'cg_update': float(o[6])}
+        d['data_rows'] = 'matrix-free' if o[7] else 'stored'
         return d
 
     def profile_kernels(self, reps=10, op=0):
@@ -129,7 +130,7 @@ def cpu_baseline(fs, b_weighted, sample_iters, threads):
 # kernel symbols per role: LSQR (assembled-SELL operator / structured stencil operator), CGNR
 # (a role's launches per iteration: its PMC bytes are the sum over the symbols found)
 KERNEL_SYMBOL = {0: {'xw_spmv': ('k_xw_spmv(', 'k_mf_fwd('), 'spmtv': ('k_spmtv(', 'k_mf_spmtv(')},
-                 1: {'cg_data': ('k_cg_data(', 'k_cg_atdq('),
+                 1: {'cg_data': ('k_cg_data(', 'k_cg_atdq(', 'k_cg_dmf_ad(', 'k_cg_dmf_atq('),
                      'cg_normal': ('k_cg_normal(', 'k_cg_normal_col<', 'k_cg_xedge('),
                      'cg_update': ('k_cg_block<', 'k_cg_jacobi(')}}
 

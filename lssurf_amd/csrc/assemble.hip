@@ -12,6 +12,8 @@
 // (count, fill) around an exclusive scan.  Compiled with -ffp-contract=off: the weights are
 // bit-identical to numpy's.
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "../../include/lsqsurf.h"
@@ -361,6 +363,81 @@ void form_from_stencils(System& S, int64_t m, int64_t n_full, int32_t n_grids, c
     S.n_sorted_rows = npts;   // data rows: point order is random in space
     S.mf = !S.dist && describe_stencil_operator(S.mfh, m, n_full, n_grids, grids, npts, n_stencil, st);
     finish_formation(S);
+    if (S.mf) build_dmf(S, n_grids, grids, n_interp, interp_grid, npts, py, px, pt);
+}
+
+// Matrix-free CGNR data rows (DmfDesc): eligible when every interpolation grid is 2-D or 3-D on one
+// shared (y, x) lattice (≤ 2 2-D parts, ≤ 1 3-D part with ≤ CG_MAXT t nodes).  The float
+// subscripts are computed here exactly as k_gen_rows computes them (one IEEE division each), the
+// points counting-sorted by (y, x) cell (stable: data-row order within a cell).
+void build_dmf(System& S, int32_t n_grids, const lsq_grid_desc* grids, int32_t n_interp, const int32_t* interp_grid,
+               int64_t npts, const double* py, const double* px, const double* pt) {
+    S.dmf = DmfDesc{};
+    if (const char* e = getenv("LSQ_CG_DMF"))
+        if (e[0] == '0') return;
+    if (n_interp < 1 || npts < 1 || npts >= (int64_t(1) << 31)) return;
+    const lsq_grid_desc& g0 = grids[interp_grid[0]];
+    DmfDesc D{};
+    const lsq_grid_desc* g3 = nullptr;
+    for (int k = 0; k < n_interp; ++k) {
+        const lsq_grid_desc& g = grids[interp_grid[k]];
+        if (g.ndim < 2 || g.ndim > 3) return;
+        for (int d = 0; d < 2; ++d)
+            if (g.shape[d] != g0.shape[d] || g.b0[d] != g0.b0[d] || g.delta[d] != g0.delta[d]) return;
+        if (g.ndim == 2) {
+            if (D.n2 == 2) return;
+            D.col2[D.n2++] = g.col0;
+        } else {
+            if (D.n3 == 1 || g.shape[2] < 2 || g.shape[2] > CG_MAXT) return;
+            D.col3 = g.col0;
+            D.n3 = 1;
+            g3 = &g;
+        }
+    }
+    if (g0.shape[0] < 2 || g0.shape[1] < 2 || (int64_t)g0.shape[0] * g0.shape[1] >= (int64_t(1) << 31)) return;
+    D.S0 = (int32_t)g0.shape[0];
+    D.S1 = (int32_t)g0.shape[1];
+    D.S2 = g3 ? (int32_t)g3->shape[2] : 1;
+    D.npts = npts;
+    const int64_t C1 = D.S1 - 1, ncell = (int64_t)(D.S0 - 1) * C1;
+    auto cell = [](double f, int S) {   // as the kernels: floor, clamped to the last cell
+        const int c = (int)std::floor(f);
+        return std::min(std::max(c, 0), S - 2);
+    };
+    std::vector<double> F(3 * npts);
+    std::vector<int64_t> key(npts);
+    std::vector<int32_t> cnt(ncell + 1, 0);
+    for (int64_t r = 0; r < npts; ++r) {
+        const double fy = (py[r] - g0.b0[0]) / g0.delta[0], fx = (px[r] - g0.b0[1]) / g0.delta[1];
+        const double ft = g3 ? (pt[r] - g3->b0[2]) / g3->delta[2] : 0.0;
+        if (!(fy >= 0.0 && fy <= D.S0 - 1 && fx >= 0.0 && fx <= D.S1 - 1)) return;   // formation rejected it
+        if (g3 && !(ft >= 0.0 && ft <= D.S2 - 1)) return;
+        F[3 * r] = fy;
+        F[3 * r + 1] = fx;
+        F[3 * r + 2] = ft;
+        key[r] = (int64_t)cell(fy, D.S0) * C1 + cell(fx, D.S1);
+        ++cnt[key[r] + 1];
+    }
+    for (int64_t c = 0; c < ncell; ++c) cnt[c + 1] += cnt[c];
+    std::vector<int32_t> perm(npts), slot(cnt.begin(), cnt.end() - 1);
+    std::vector<double> P(4 * npts);
+    for (int64_t r = 0; r < npts; ++r) {
+        const int32_t i = slot[key[r]]++;
+        perm[i] = (int32_t)r;
+        P[4 * i] = F[3 * r];
+        P[4 * i + 1] = F[3 * r + 1];
+        P[4 * i + 2] = F[3 * r + 2];
+        P[4 * i + 3] = 1.0;   // row scale, refreshed per solve (cg_dmf_prepare)
+    }
+    S.dmf_pt.alloc(4 * npts);
+    S.dmf_pt.upload(P.data(), 4 * npts, S.stream);
+    S.dmf_perm.alloc(npts);
+    S.dmf_perm.upload(perm.data(), npts, S.stream);
+    S.dmf_cell.alloc(ncell + 1);
+    S.dmf_cell.upload(cnt.data(), ncell + 1, S.stream);
+    HIP_CHECK(hipStreamSynchronize(S.stream));
+    D.ok = 1;
+    S.dmf = D;
 }
 
 }  // namespace lsq

@@ -652,6 +652,7 @@ void build_stencil_operator(System& S) {
 }  // namespace
 
 void finish_formation(System& S) {
+    S.dmf = DmfDesc{};
     hipStream_t st = S.stream;
     Csr& G = S.G;
     const int64_t m = G.m, n = G.n;
@@ -787,6 +788,7 @@ void referenced_cols(System& S, uint8_t* h_flags) {
 }
 
 void relabel_columns(System& S, const int32_t* h_map, int64_t n_local) {
+    S.dmf.ok = 0;   // the matrix-free data rows address the formation's column space
     DBuf<int32_t> map(std::max<int64_t>(S.G.n, 1));
     map.upload(h_map, S.G.n, S.stream);
     DBuf<unsigned long long> bad(1);

@@ -163,6 +163,16 @@ struct CgDesc {
     int32_t nedge, maxt3, pad[2];            // column mode: workgroups of k_cg_xedge; 3-D column length
     CgGrid g[MF_MAX_GRIDS];
 };
+// CGNR data rows without a stored matrix (lsqr_cg.inc, k_cg_dmf_*): when every interpolation
+// grid shares one (y, x) node lattice (and the 3-D ones one t lattice), a data row is fully given
+// by its point's float subscripts f_d = (p_d − b0_d)/δ_d (the values lin_op.interp_mtx and
+// k_gen_rows derive the weights from) and its row scale.  Points are stored sorted by (y, x)
+// cell; cell_ptr gives each cell's run, so AdᵀAd gathers per node without a transpose.
+struct DmfDesc {
+    int32_t ok, n2, n3, S0, S1, S2;   // 2-D / 3-D parts; lattice shape (S2: t nodes of the 3-D part)
+    int64_t npts;
+    int64_t col2[2], col3;            // col0 of the 2-D parts' grids and of the 3-D part's grid
+};
 // PCG-on-AᵀA scalar state (device resident).  Quantities are those of CGLS on A·M^{-1/2}; the
 // LSQR estimates (anorm, xnorm of the correction, ‖r‖, ‖Aᵀr‖) follow from the CG scalars through
 // the Lanczos relation.
@@ -257,6 +267,9 @@ struct System {
     // row scales change; vectors in the full column space
     bool cg_ok = false;            // the structured normal operator exists for this system
     int64_t cg_data_cols = 0;      // columns touched by the data rows
+    DmfDesc dmf{};                  // matrix-free data rows for CGNR (ok = 0: use Ad / ATd)
+    DBuf<double> dmf_pt;            // per sorted point: f_y, f_x, f_t, row scale (double4)
+    DBuf<int32_t> dmf_perm, dmf_cell;   // sorted point -> data row; (y, x) cell -> first sorted point
     std::string cg_why;            // why not (when !cg_ok)
     CgDesc cgh{};
     DBuf<CgDesc> cgd;
@@ -303,6 +316,8 @@ void relabel_columns(System& S, const int32_t* h_map, int64_t n_local);
 void form_from_coo(System& S, int64_t m, int64_t n_full, int64_t nnz, const int64_t* r,
                    const int64_t* c, const double* v);
 void finish_formation(System& S);              // G set -> GT, SELL copies, default scaling
+void build_dmf(System& S, int32_t n_grids, const lsq_grid_desc* grids, int32_t n_interp, const int32_t* interp_grid,
+               int64_t npts, const double* py, const double* px, const double* pt);   // S.dmf (CGNR data rows)
 void ensure_sell(System& S);                    // assembled A / AT (lazy when S.mf)
 void refresh_scaling(System& S, int precond);   // rs/cs -> SELL values (single GPU)
 void scaling_rows_colnorm(System& S, int precond, bool raw);

@@ -171,6 +171,7 @@ class LSQSolver:
         self._check(self._L.lsq_profile_cg(self._h, int(reps), int(precond), ptr(o)), 'lsq_profile_cg')
         d = dict(zip(['cg_data', 'cg_normal', 'cg_update', 'cg_scalars'], o[:4].tolist()))
         d['bytes'] = {'cg_data': float(o[4]), 'cg_normal': float(o[5]), 'cg_update': float(o[6])}
+        d['data_rows'] = 'matrix-free' if o[7] else 'stored'
         return d
 
     def normal_apply(self, p_full):

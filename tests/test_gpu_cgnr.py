@@ -220,3 +220,33 @@ def test_cgnr_2d_lin_op_system_exact_solution(gpu_available):
     xs = g['x']
     assert np.linalg.norm(x - xs) / np.linalg.norm(xs) <= REL
     assert np.max(np.abs(x - xs)) <= ABS
+
+
+@pytest.mark.parametrize('which', ['t64', 'nb_xt'])
+def test_matrix_free_data_rows_match_stored_rows(gpu_available, which, monkeypatch):
+    """CGNR's matrix-free data rows (point subscripts sorted by cell, k_cg_dmf_*) against the
+    stored Ad / ATd path (LSQ_CG_DMF=0, read at formation): same AᵀA p to rounding, same solve."""
+    out = {}
+    for flag in ('1', '0'):
+        monkeypatch.setenv('LSQ_CG_DMF', flag)
+        if which == 't64':
+            S, fs, w, rhs = _synthetic_system(which)
+        else:
+            g, fs, w, rhs = _golden_system(which)
+        keep = np.random.default_rng(5).random(fs.n_data) > 0.2
+        try:
+            fs.solver.set_row_weight(w)
+            fs.solver.set_row_mask(np.concatenate([keep, np.ones(fs.n_con, bool)]))
+            pf = np.zeros(fs.n_full)
+            pf[fs.keep_cols] = np.random.default_rng(9).standard_normal(fs.keep_cols.size)
+            q = fs.solver.normal_apply(pf)[fs.keep_cols]
+            mode = fs.solver.profile_cg(reps=1)['data_rows']
+            x = fs.solve(w, keep, rhs, precond=3, method=1, **TOL)
+            out[flag] = (q, x, fs.stats['iters'], mode)
+        finally:
+            fs.close()
+    (q1, x1, i1, m1), (q0, x0, i0, m0) = out['1'], out['0']
+    assert m0 == 'stored' and (m1 == 'matrix-free' or which != 't64'), (m1, m0)
+    assert np.abs(q1 - q0).max() <= 1e-12 * np.abs(q0).max()
+    assert np.linalg.norm(x1 - x0) <= 1e-9 * np.linalg.norm(x0)
+    assert abs(i1 - i0) <= 2, (i1, i0)
