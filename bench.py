@@ -130,7 +130,7 @@ def cpu_baseline(fs, b_weighted, sample_iters, threads):
 # kernel symbols per role: LSQR (assembled-SELL operator / structured stencil operator), CGNR
 # (a role's launches per iteration: its PMC bytes are the sum over the symbols found)
 KERNEL_SYMBOL = {0: {'xw_spmv': ('k_xw_spmv(', 'k_mf_fwd('), 'spmtv': ('k_spmtv(', 'k_mf_spmtv(')},
-                 1: {'cg_data': ('k_cg_data(', 'k_cg_atdq(', 'k_cg_dmf_ad(', 'k_cg_dmf_atq('),
+                 1: {'cg_data': ('k_cg_data(', 'k_cg_atdq(', 'k_cg_dmf_ad(', 'k_cg_dmf_atq<'),
                      'cg_normal': ('k_cg_normal(', 'k_cg_normal_col<', 'k_cg_xedge('),
                      'cg_update': ('k_cg_block<', 'k_cg_jacobi(')}}
 
@@ -302,6 +302,7 @@ def main():
         roles = ('spmtv', 'xw_spmv')
     # algorithmic bytes per launch (DESIGN.md §Byte model)
     kb = prof.pop('bytes')   # algorithmic bytes per launch, from the library's byte model
+    data_rows = prof.pop('data_rows', None)   # CGNR: 'matrix-free' (points sorted by cell) or 'stored'
     dom = max(roles, key=lambda k: prof[k])
     achieved = kb[dom] / (prof[dom] * 1e-3) / 1e9
 
@@ -339,7 +340,8 @@ def main():
             'config': {'workload': f'{"2-D lin_op (z0 only)" if args.config in ("c2", "t2d") else "smooth_fit"} solve, {args.config}',
                        'rank0_system': info, 'rows': gm, 'cols': gn,
                        'nnz': gZ, 'precond': {1: 'column scaling', 3: 'block-Jacobi per (y,x) node'}.get(args.precond, args.precond),
-                       'operator': 'structured stencil rows + SELL data rows'
+                       'operator': ('structured stencil rows + ' + ('matrix-free data rows (points sorted by cell)'
+                                                                     if data_rows == 'matrix-free' else 'SELL data rows'))
                        if (fs.structured if isinstance(solver, _Dist) else info.get('stencil_op') and args.op == 0)
                        else 'assembled SELL',
                        'parallelism': f'y-slab rows x{world} (RCCL)' if world > 1 or args.dist else 'single'},
