@@ -161,8 +161,14 @@ __global__ __launch_bounds__(BLOCK) void k_spmtv(const LsqState* __restrict__ st
 // deterministic single-block sum of nparts partials
 __device__ double reduce_parts(const double* part, int nparts) {
     __shared__ double red[4];
-    double a = 0.0;
-    for (int i = threadIdx.x; i < nparts; i += BLOCK) a += part[i];
+    double a = 0.0;   // same summation order as a plain strided loop, 8 loads in flight
+    for (int i0 = threadIdx.x; i0 < nparts; i0 += 8 * BLOCK) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = i0 + u * BLOCK < nparts ? part[i0 + u * BLOCK] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a += v[u];
+    }
     return block_sum(a, red);  // valid in thread 0
 }
 
