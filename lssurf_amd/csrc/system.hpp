@@ -183,6 +183,10 @@ struct CgState {
     double r1norm, arnorm, xnorm, anorm;
     int64_t itn, maxit;
     int32_t istop, stop, no_stop, pad;
+    // x is updated every other iteration: x += α_{k−1}p_{k−1} + α_k p_k (p_{k−1} is still the
+    // other ping-pong buffer); pend = 1 while α_k p_k is owed (pend_buf: which buffer holds p_k)
+    int32_t pend, pend_buf;
+    double pend_alpha;
 };
 
 struct System {
