@@ -811,6 +811,9 @@ void relabel_columns(System& S, const int32_t* h_map, int64_t n_local) {
 
 System::~System() {
     if (comm) (void)ncclCommDestroy(comm);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (side) (void)hipStreamDestroy(side);
     if (stream && own_stream) (void)hipStreamDestroy(stream);
 }
 

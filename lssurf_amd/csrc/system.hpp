@@ -252,6 +252,8 @@ struct System {
     bool dist = false;
     bool virt = false;              // in-process virtual rank (shares device + stream with its group)
     bool own_stream = true;
+    hipStream_t side = nullptr;              // CGNR: k_cg_xedge beside the data kernel (fork/join events)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int rank = 0, nranks = 1;
     ncclComm_t comm = nullptr;
     int64_t n_own = 0;
