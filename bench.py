@@ -131,7 +131,7 @@ def cpu_baseline(fs, b_weighted, sample_iters, threads):
 # (a role's launches per iteration: its PMC bytes are the sum over the symbols found)
 KERNEL_SYMBOL = {0: {'xw_spmv': ('k_xw_spmv(', 'k_mf_fwd('), 'spmtv': ('k_spmtv(', 'k_mf_spmtv(')},
                  1: {'cg_data': ('k_cg_data(', 'k_cg_atdq(', 'k_cg_dmf_ad(', 'k_cg_dmf_atq<'),
-                     'cg_normal': ('k_cg_normal(', 'k_cg_normal_col<', 'k_cg_xedge('),
+                     'cg_normal': ('k_cg_normal(', 'k_cg_normal_col<', 'k_cg_xedge<'),
                      'cg_update': ('k_cg_block<', 'k_cg_jacobi(')}}
 
 
@@ -315,7 +315,7 @@ def main():
                  'solve_method': ['lsqr', 'cgnr'][int(sst.get('method', 0))],
                  'solve_precond': {1: 'column scaling', 3: 'block-Jacobi per (y,x) node'}.get(args.precond, args.precond)}
         if meth == 1 and not isinstance(solver, _Dist):   # distributed LSQR has no block-Jacobi
-            xl, sl = solver.solve(rhs, op=args.op, precond=args.precond, method=0)
+            xl, sl = solver.solve(rhs, op=args.op, precond=min(args.precond, 3), method=0)
             solve['solve_lsqr'] = {'solve_time_s': sl['time_s'], 'solve_iters': int(sl['iters']),
                                    'solve_istop': int(sl['istop'])}
             solve['solve_rel_diff_vs_lsqr'] = float(np.linalg.norm(x - xl) / np.linalg.norm(xl))

@@ -50,7 +50,10 @@ typedef struct lsq_opts {
     int32_t precond;       /* 0 = none, 1 = column (Jacobi) scaling, 2 = dense Cholesky R⁻¹   */
                            /*     (exact right preconditioner; n up to a few 10^4), 3 = block-  */
                            /*     Jacobi: R_b⁻¹ of every column block (lsq_set_column_blocks;   */
-                           /*     SURVEY.md §8 a7.4 — no reference counterpart)                 */
+                           /*     SURVEY.md §8 a7.4 — no reference counterpart), 4 = geometric  */
+                           /*     multigrid V-cycle over the (y, x) node lattice (method 1,     */
+                           /*     single-GPU smooth_fit systems with per-node column blocks;    */
+                           /*     DESIGN.md §Multigrid)                                         */
     double  atol, btol, conlim;
     int64_t maxit;
     int32_t use_x0;        /* 1: x_inout holds a warm start (outer-iteration "resume")          */
@@ -69,6 +72,9 @@ typedef struct lsq_stats {
     double  r1norm, r2norm, anorm, acond, arnorm, xnorm;
     double  time_s;        /* device-resident iteration time (A, b already in HBM)              */
     double  bytes_per_iter;/* algorithmic HBM bytes of one LSQR iteration (DESIGN.md byte model)*/
+    double  setup_s;       /* CGNR: per-solve preconditioner set-up and initialisation (block   */
+                           /*     factors, multigrid levels and λ estimates), host wall clock, */
+                           /*     not part of time_s; LSQR: 0                                  */
 } lsq_stats;
 
 void        lsq_default_opts(lsq_opts* o);
@@ -233,6 +239,14 @@ int lsq_profile_kernels(lsq_handle* h, int32_t reps, int32_t op, double* out8);
  * space (length n_full of lsq_set_col_map; test hook for the normal operator). */
 int lsq_cg_available(lsq_handle* h, int32_t precond);
 int lsq_profile_cg(lsq_handle* h, int32_t reps, int32_t precond, double* out8);
+/* Multigrid (precond 4) test hooks.  lsq_mg_info: out[0] = levels L, then per level
+ * (S0, S1, n_full, removed epoch) — cap must hold 1 + 4L values.  lsq_mg_apply on level l's full
+ * column space (z0 grid then dz grid, in the system's order): what 0: y = N_l x (level 0: AᵀA;
+ * coarse levels: Galerkin PᵀNP of the stencil rows + the (y, x)-lumped data rows), 1: y = the
+ * V-cycle applied to x (level 0), 2: y[0] = the smoother's λ_max(M⁻¹N) estimate of level l.
+ * Both build the hierarchy for the current row weights / mask. */
+int lsq_mg_info(lsq_handle* h, int64_t* out, int64_t cap);
+int lsq_mg_apply(lsq_handle* h, int32_t level, int32_t what, const double* x, double* y);
 int lsq_normal_apply(lsq_handle* h, const double* p, double* q);
 int lsq_sell_info(lsq_handle* h, int64_t* out8);
 

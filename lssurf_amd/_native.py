@@ -35,7 +35,7 @@ class LsqStats(ctypes.Structure):
     _fields_ = [('iters', ctypes.c_int64), ('istop', ctypes.c_int32), ('method', ctypes.c_int32),
                 ('r1norm', ctypes.c_double), ('r2norm', ctypes.c_double), ('anorm', ctypes.c_double),
                 ('acond', ctypes.c_double), ('arnorm', ctypes.c_double), ('xnorm', ctypes.c_double),
-                ('time_s', ctypes.c_double), ('bytes_per_iter', ctypes.c_double)]
+                ('time_s', ctypes.c_double), ('bytes_per_iter', ctypes.c_double), ('setup_s', ctypes.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -45,7 +45,7 @@ class LsqStats(ctypes.Structure):
 EXPORTS = ['lsq_default_opts', 'lsq_create', 'lsq_destroy', 'lsq_last_error', 'lsq_set_col_map',
            'lsq_set_matrix_coo', 'lsq_set_matrix_stencil', 'lsq_set_row_weight', 'lsq_set_row_mask',
            'lsq_set_column_blocks', 'lsq_shape', 'lsq_get_csr',
-           'lsq_solve', 'lsq_spmv', 'lsq_spmv_rows', 'lsq_iterate', 'lsq_profile_kernels', 'lsq_cg_available', 'lsq_profile_cg', 'lsq_normal_apply', 'lsq_sell_info', 'lsq_sigma_x',
+           'lsq_solve', 'lsq_spmv', 'lsq_spmv_rows', 'lsq_iterate', 'lsq_profile_kernels', 'lsq_cg_available', 'lsq_profile_cg', 'lsq_mg_info', 'lsq_mg_apply', 'lsq_normal_apply', 'lsq_sell_info', 'lsq_sigma_x',
            'lsq_get_rinv', 'lsq_dist_unique_id', 'lsq_create_dist', 'lsq_dist_referenced_cols',
            'lsq_dist_set_layout', 'lsq_dist_set_halo', 'lsq_vgroup_create', 'lsq_vgroup_rank', 'lsq_vgroup_solve', 'lsq_vgroup_iterate',
            'lsq_vgroup_last_error', 'lsq_vgroup_destroy',
@@ -84,6 +84,8 @@ def load():
         'lsq_profile_kernels': ([P, i32, i32, P], ctypes.c_int),
         'lsq_cg_available': ([P, i32], ctypes.c_int),
         'lsq_profile_cg': ([P, i32, i32, P], ctypes.c_int),
+        'lsq_mg_info': ([P, P, i64], ctypes.c_int),
+        'lsq_mg_apply': ([P, i32, i32, P, P], ctypes.c_int),
         'lsq_normal_apply': ([P, P, P], ctypes.c_int),
         'lsq_sell_info': ([P, P], ctypes.c_int),
         'lsq_sigma_x': ([P, P], ctypes.c_int),

@@ -1,5 +1,6 @@
 // api.hip — extern "C" entry points of liblsqsurf.so (declared in include/lsqsurf.h).
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <vector>
 
@@ -253,7 +254,10 @@ int lsq_solve(lsq_handle* h, const double* b, double* x_inout, const lsq_opts* o
         lsq_default_opts(&d);
         if (!o) o = &d;
         if (o->method != 0 && o->method != 1) return fail(S, "lsq_solve: method must be 0 (LSQR) or 1 (CGNR)");
-        if (o->precond < 0 || o->precond > 3) return fail(S, "lsq_solve: precond must be 0, 1, 2 or 3");
+        if (o->precond < 0 || o->precond > 4) return fail(S, "lsq_solve: precond must be 0, 1, 2, 3 or 4");
+        if (o->precond == 4 && (o->method != 1 || S.dist || !lsq::cg_available(S, 4)))
+            return fail(S, "lsq_solve: precond 4 (multigrid) runs CGNR (method 1) on single-GPU structured systems: " +
+                               (S.dist ? std::string("distributed rank") : o->method != 1 ? std::string("method is not 1") : S.cg_ok ? S.mg_why : S.cg_why));
         if (S.dist) {
             if (S.virt) return fail(S, "lsq_solve: a virtual rank solves through lsq_vgroup_solve");
             lsq::Group G;
@@ -261,8 +265,18 @@ int lsq_solve(lsq_handle* h, const double* b, double* x_inout, const lsq_opts* o
             double* xs[1] = {x_inout};
             return o->method == 1 ? lsq::group_cg_solve(G, &b, xs, *o, s) : lsq::group_solve(G, &b, xs, *o, s);
         }
-        if (o->method == 1 && lsq::cg_available(S, o->precond)) return lsq::cg_solve(S, b, x_inout, *o, s);
-        if (s) s->method = 0;
+        const auto t_prep = std::chrono::steady_clock::now();
+        if (o->method == 1 && lsq::cg_available(S, o->precond)) {   // builds block factors / levels when stale
+            HIP_CHECK(hipStreamSynchronize(S.stream));
+            const double prep_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_prep).count();
+            const int rc = lsq::cg_solve(S, b, x_inout, *o, s);
+            if (s) s->setup_s += prep_s;
+            return rc;
+        }
+        if (s) {
+            s->method = 0;
+            s->setup_s = 0.0;
+        }
         return lsq::lsqr_solve(S, b, x_inout, *o, s);
     });
 }
@@ -273,6 +287,9 @@ int lsq_iterate(lsq_handle* h, const double* b, int64_t iters, const lsq_opts* o
         lsq_opts d;
         lsq_default_opts(&d);
         if (!o) o = &d;
+        if (o->precond == 4 && (o->method != 1 || S.dist || !lsq::cg_available(S, 4)))
+            return fail(S, "lsq_iterate: precond 4 (multigrid) runs CGNR (method 1) on single-GPU structured systems: " +
+                               (S.dist ? std::string("distributed rank") : o->method != 1 ? std::string("method is not 1") : S.cg_ok ? S.mg_why : S.cg_why));
         if (S.dist) {
             if (S.virt) return fail(S, "lsq_iterate: a virtual rank iterates through lsq_vgroup_iterate");
             lsq::Group G;
@@ -288,12 +305,12 @@ int lsq_iterate(lsq_handle* h, const double* b, int64_t iters, const lsq_opts* o
 int lsq_cg_available(lsq_handle* h, int32_t precond) {
     return guarded(h, [&](lsq::System& S) {
         if (!S.G.rp.p) return fail(S, "lsq_cg_available: no matrix");
-        if (precond != 1 && precond != 3) {
-            S.err = "CGNR runs with precond 1 (Jacobi) or 3 (block-Jacobi)";
+        if (precond != 1 && precond != 3 && precond != 4) {
+            S.err = "CGNR runs with precond 1 (Jacobi), 3 (block-Jacobi) or 4 (multigrid)";
             return 0;
         }
         if (lsq::cg_available(S, precond)) return 1;
-        S.err = S.cg_why.empty() ? "not a structured single-GPU system" : S.cg_why;
+        S.err = !S.cg_ok ? (S.cg_why.empty() ? "not a structured single-GPU system" : S.cg_why) : S.mg_why;
         return 0;
     });
 }
@@ -305,6 +322,23 @@ int lsq_profile_cg(lsq_handle* h, int32_t reps, int32_t precond, double* out8) {
         if (!lsq::cg_available(S, precond)) return fail(S, "lsq_profile_cg: CGNR not available: " + S.cg_why);
         lsq::graph_cache_drop(&S);
         lsq::cg_profile(S, reps > 0 ? reps : 10, precond, out8);
+        return 0;
+    });
+}
+
+int lsq_mg_info(lsq_handle* h, int64_t* out, int64_t cap) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_mg_info: no matrix");
+        if (!out) return fail(S, "lsq_mg_info: null output");
+        return lsq::mg_info(S, out, cap);
+    });
+}
+
+int lsq_mg_apply(lsq_handle* h, int32_t level, int32_t what, const double* x, double* y) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_mg_apply: no matrix");
+        if (!y || (what != 2 && !x)) return fail(S, "lsq_mg_apply: null vector");
+        lsq::mg_test_apply(S, level, what, x, y);
         return 0;
     });
 }

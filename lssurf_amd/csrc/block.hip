@@ -233,4 +233,16 @@ void block_factor(System& S) {
     block_factor_in_place(S);
 }
 
+// Multigrid coarse levels (mg.inc): nb packed blocks (AᵀA)_bb of kmax columns in Ri -> R_b⁻¹ in
+// place, then the fp32 copy Lf (block stride npks = npk rounded up to even).  ptr: device block
+// pointers (b·kmax).  Asynchronous on `st`.
+void block_factor_packed(int64_t nb, const int64_t* ptr, int kmax, double* Ri, float* Lf,
+                         unsigned long long* ndead, hipStream_t st) {
+    hipLaunchKernelGGL(k_block_factor, dim3(grid_for(nb)), dim3(BLOCK), 0, st, nb, ptr, kmax, Ri, ndead);
+    KERNEL_CHECK();
+    const int npk = kmax * (kmax + 1) / 2, npks = (npk + 1) & ~1;
+    hipLaunchKernelGGL(k_block_rinv32, dim3(grid_for(nb * npks)), dim3(BLOCK), 0, st, nb, npk, npks, Ri, Lf);
+    KERNEL_CHECK();
+}
+
 }  // namespace lsq

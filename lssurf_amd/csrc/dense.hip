@@ -337,6 +337,30 @@ void dense_factor(System& S) {
     S.dense_valid = true;
 }
 
+// In place: Nm (npad x npad, row-major, SPD on its upper triangle, identity on the padding) -> R
+// (upper Cholesky factor), and Ri = R⁻¹.  err (device int) is set when a pivot is not positive.
+// Asynchronous on `st` (multigrid coarsest level, mg.inc).
+void dense_spd_factor(double* Nm, double* Ri, int64_t npad, int* err, hipStream_t st) {
+    const int64_t ld = npad;
+    const int nb = (int)(npad / TB);
+    HIP_CHECK(hipMemsetAsync(Ri, 0, sizeof(double) * (size_t)(npad * npad), st));
+    for (int kb = 0; kb < nb; ++kb) {
+        const int64_t k0 = (int64_t)kb * TB;
+        hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(BLOCK), 0, st, Nm, ld, k0, err);
+        const int m = nb - kb - 1;
+        if (m > 0) {
+            hipLaunchKernelGGL(k_trsm_panel, dim3(m), dim3(BLOCK), 0, st, Nm, ld, k0);
+            hipLaunchKernelGGL(k_syrk_tiles, dim3(m * m), dim3(BLOCK), 0, st, Nm, ld, k0, m);
+        }
+    }
+    hipLaunchKernelGGL(k_zero_lower, dim3(grid_for(npad * npad)), dim3(BLOCK), 0, st, Nm, npad, ld);
+    for (int ib = nb - 1; ib >= 0; --ib) {
+        hipLaunchKernelGGL(k_trinv_diag, dim3(1), dim3(BLOCK), 0, st, Nm, Ri, ld, (int64_t)ib * TB);
+        if (nb - 1 - ib > 0) hipLaunchKernelGGL(k_trinv_row, dim3(nb - 1 - ib), dim3(BLOCK), 0, st, Nm, Ri, ld, ib);
+    }
+    KERNEL_CHECK();
+}
+
 void dense_rowrss(System& S, double* dE) {
     const int64_t n = S.G.n;
     hipLaunchKernelGGL(k_rowrss_dense, dim3((unsigned)((n + 3) / 4)), dim3(BLOCK), 0, S.stream, S.dRi.p, n,

@@ -14,6 +14,8 @@
 // values (A·D), and x = D y is applied on the way out.
 #include <array>
 #include <chrono>
+#include <memory>
+#include <stdexcept>
 #include <cmath>
 #include <vector>
 

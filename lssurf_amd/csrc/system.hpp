@@ -14,6 +14,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <string>
 #include <vector>
 
@@ -125,7 +126,7 @@ struct LsqState {
 // dim 2 are staged in LDS with their halo; lane = dim-1 position, so a wave's class is uniform
 // except on tiles at a dim-1 edge.
 constexpr int CG_TX = 64;
-constexpr int CG_MAX_OFF = 64;
+constexpr int CG_MAX_OFF = 128;             // Galerkin coarse grids (mg.inc): 5×5 (dy, dx) × 5 dt
 constexpr int CG_MAXI = 16;                 // (row, dim-2) items per wave of one tile
 // Column mode (every grid: dim 2 ≤ CG_MAXT nodes, |dt| ≤ 2): a thread owns a whole dim-2 column
 // (y, x, 0..S2−1) and accumulates it in registers; the normal stencil is walked as (dy, dx)
@@ -158,9 +159,27 @@ struct CgGrid {
 struct BlkAffine {
     int64_t base[16], stride[16];
 };
+// Normal stencil of one grid on the host: (AᵀA) of the grid's stencil rows as a class table,
+// coef[((cy·ncls1 + cx)·ncls2 + ct)·noff + o] = (AᵀA)_{c, c + offs[o]} at every node c of class
+// (cy, cx, ct).  Built from the stencil parts (lsqr_cg.inc ns_from_parts) or, on a multigrid
+// coarse level, as the Galerkin product PᵀNP of the finer level's table (mg.inc).
+struct NsTable {
+    bool on = false;
+    int shape[3] = {1, 1, 1};
+    int K[3] = {0, 0, 0}, ncls[3] = {1, 1, 1};
+    int64_t col0 = 0;
+    int node0 = 0;
+    std::vector<std::array<int, 3>> offs;   // sorted
+    std::vector<double> coef;
+    const double* row(int cy, int cx, int ct) const {
+        return coef.data() + ((size_t)(cy * ncls[1] + cx) * ncls[2] + ct) * offs.size();
+    }
+};
+struct MgHier;   // multigrid hierarchy (mg.inc)
+void mg_free(MgHier* h);
 struct CgDesc {
     int32_t n_grids, ntiles, lds_max, colmode;
-    int32_t nedge, maxt3, pad[2];            // column mode: workgroups of k_cg_xedge; 3-D column length
+    int32_t nedge, maxt3, pad[2];            // column mode: workgroups of k_cg_xedge<1> (pad[0]: <8>); 3-D column length
     CgGrid g[MF_MAX_GRIDS];
 };
 // CGNR data rows without a stored matrix (lsqr_cg.inc, k_cg_dmf_*): when every interpolation
@@ -280,6 +299,9 @@ struct System {
     CgDesc cgh{};
     DBuf<CgDesc> cgd;
     DBuf<double> cg_coef, cg_coefc;  // class-row tables: offset-major (tile mode), group × t (column mode)
+    std::vector<NsTable> cg_ns;      // host copy of each grid's normal-stencil table (multigrid input)
+    MgHier* mg = nullptr;            // precond 4: geometric multigrid levels (mg.inc), built lazily
+    std::string mg_why;              // why precond 4 is unavailable
     std::vector<double> cg_wkey;   // part row scales the table was built for
     DBuf<double> cg_x, cg_s, cg_z, cg_p0, cg_p1, cg_q, cg_t, cg_part_g, cg_part_r, cg_part_t;
     DBuf<CgState> cst;
@@ -340,10 +362,17 @@ void ensure_blocks(System& S);                     // default structure if none 
 void block_factor(System& S);                      // R_b⁻¹ for the current row scale
 void block_normal(System& S);                      // (AᵀA)_bb of the system's own rows into blk_Ri
 void block_factor_in_place(System& S);             // blk_Ri: (AᵀA)_bb -> R_b⁻¹
+void block_factor_packed(int64_t nb, const int64_t* ptr, int kmax, double* Ri, float* Lf,
+                         unsigned long long* ndead, hipStream_t st);   // multigrid coarse blocks
 
 // dense.hip
 void dense_factor(System& S);                     // R, R⁻¹ of diag(rs)·G (throws if not SPD)
 void dense_rowrss(System& S, double* dE);         // sqrt(row sums of R⁻¹²) = sqrt(diag((AᵀA)⁻¹))
+void dense_spd_factor(double* Nm, double* Ri, int64_t npad, int* err, hipStream_t st);   // multigrid coarsest
+
+// multigrid test hooks (mg.inc; lsq_mg_info / lsq_mg_apply)
+int mg_info(System& S, int64_t* out, int64_t cap);
+void mg_test_apply(System& S, int level, int what, const double* x, double* y);
 __global__ void k_gemv_upper(const double* M, int64_t n, int64_t ld, const double* v, const LsqState* st,
                              int scale_mode, double* z);
 __global__ void k_gemvT_upper(const double* M, int64_t n, int64_t ld, const double* t, const LsqState* st, int mode,

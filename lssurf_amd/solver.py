@@ -125,11 +125,13 @@ class LSQSolver:
         return sp.csr_matrix((v[:z], ci[:z], rp), shape=(m, n))
 
     # ---- solve -------------------------------------------------------------------------------
-    def solve(self, b, x0=None, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, batch=16,
+    def solve(self, b, x0=None, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, batch=0,
               use_graph=True, op=0, method=0):
         """LSQR (method 0) or CGNR (method 1: PCG on the normal equations with the fused
         normal-stencil operator; LSQR where that operator does not exist — stats['method'] says
-        which ran); returns (x, stats) with scipy-lsqr-style stats (iters, istop, r1norm, ...)."""
+        which ran); returns (x, stats) with scipy-lsqr-style stats (iters, istop, r1norm, ...).
+        precond: 1 Jacobi, 2 dense Cholesky, 3 block-Jacobi per node, 4 multigrid V-cycle (CGNR
+        only).  batch 0: the library's default iterations per host convergence check."""
         b = as_c(b, np.float64)
         if b.size != self.m:
             raise ValueError(f'b has {b.size} rows, system has {self.m}')
@@ -141,7 +143,7 @@ class LSQSolver:
         self._check(self._L.lsq_solve(self._h, ptr(b), ptr(x), ctypes.byref(o), ctypes.byref(st)), 'lsq_solve')
         return x, st.as_dict()
 
-    def iterate(self, b, iters, precond=1, batch=16, use_graph=True, op=0, method=0):
+    def iterate(self, b, iters, precond=1, batch=0, use_graph=True, op=0, method=0):
         b = as_c(b, np.float64)
         o = default_opts(precond=int(precond), batch=int(batch), use_graph=int(bool(use_graph)), op=int(op),
                          method=int(method))
@@ -173,6 +175,29 @@ class LSQSolver:
         d['bytes'] = {'cg_data': float(o[4]), 'cg_normal': float(o[5]), 'cg_update': float(o[6])}
         d['data_rows'] = 'matrix-free' if o[7] else 'stored'
         return d
+
+    def mg_info(self):
+        """Multigrid (precond 4) levels: list of (S0, S1, n_full) per level, and the removed epoch."""
+        o = np.zeros(1 + 4 * 32, np.int64)
+        self._check(self._L.lsq_mg_info(self._h, ptr(o), o.size), 'lsq_mg_info')
+        L = int(o[0])
+        return [tuple(int(v) for v in o[1 + 4 * l:4 + 4 * l]) for l in range(L)], int(o[4])
+
+    def mg_apply(self, level, what, x=None):
+        """Multigrid test hook: what 0 → N_l x on level l's full column space; 1 → V-cycle(x)
+        (level 0); 2 → the smoother's λ_max(M⁻¹N) estimate of level l."""
+        levels, _ = self.mg_info()
+        nf = levels[level][2]
+        if what == 2:
+            y = np.zeros(1)
+            self._check(self._L.lsq_mg_apply(self._h, int(level), 2, None, ptr(y)), 'lsq_mg_apply')
+            return float(y[0])
+        xx = as_c(x, np.float64)
+        if xx.size != nf:
+            raise ValueError(f'x must have {nf} entries')
+        y = np.zeros(nf)
+        self._check(self._L.lsq_mg_apply(self._h, int(level), int(what), ptr(xx), ptr(y)), 'lsq_mg_apply')
+        return y
 
     def normal_apply(self, p_full):
         """q = AᵀA p over the full column space (current weights / mask)."""

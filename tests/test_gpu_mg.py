@@ -1,0 +1,139 @@
+"""GPU parity of the multigrid preconditioner (lsq_opts.precond = 4; lssurf_amd/csrc/mg.inc).
+
+* every level operator equals the host (scipy) hierarchy built from the formed A: Galerkin
+  PᵀN_sP of the stencil rows + the (y, x)-lumped data rows (tests/mg_host.py), ≤ 1e-11 relative;
+* the V-cycle is a symmetric positive-definite operator (a valid PCG preconditioner);
+* PCG with it reaches the exact LS solution within DESIGN.md's tolerance (‖x−x*‖/‖x*‖ ≤ 1e-6,
+  max|x−x*| ≤ 1e-4 m), and in far fewer iterations than block-Jacobi."""
+import numpy as np
+import pytest
+
+from conftest import golden
+from mg_host import hierarchy
+from test_gpu_cgnr import REL, ABS, TOL, _golden_system, _synthetic_system
+
+pytestmark = pytest.mark.gpu
+
+
+def _prepare(fs, w, keep):
+    fs.solver.set_row_weight(w)
+    fs.solver.set_row_mask(np.concatenate([keep, np.ones(fs.n_con, bool)]))
+    ok, why = fs.solver.cg_available(4)
+    assert ok, why
+
+
+@pytest.mark.parametrize('which', ['t64', 't15', 'tdense'])
+def test_mg_level_operators_match_host_galerkin(gpu_available, which):
+    S, fs, w, rhs = _synthetic_system(which)
+    rng = np.random.default_rng(11)
+    keep = rng.random(fs.n_data) > 0.15          # edited data rows, as the outer loop sets
+    try:
+        _prepare(fs, w, keep)
+        levels, tref = fs.solver.mg_info()
+        A = fs.solver.get_csr()
+        ny, nx, nt = S['grids']['dz'].shape
+        host = hierarchy(A, int(keep.sum()), fs.keep_cols, ny, nx, nt)
+        assert len(host) == len(levels), (len(host), levels)
+        for l, ((shape, kmask, N), (S0, S1, nf)) in enumerate(zip(host, levels)):
+            assert shape == (S0, S1) and nf == kmask.size
+            if l == len(levels) - 1:
+                break                                # coarsest: dense inverse, no operator kernel
+            for _ in range(2):
+                x = np.where(kmask, rng.standard_normal(nf), 0.0)
+                y = fs.solver.mg_apply(l, 0, x)
+                yr = N @ x
+                err = np.abs(y - yr).max() / np.abs(yr).max()
+                assert err <= 1e-11, (l, err)
+                assert np.all(y[~kmask] == 0.0)
+            lam = fs.solver.mg_apply(l, 2)
+            assert np.isfinite(lam) and lam > 0.5, (l, lam)
+    finally:
+        fs.close()
+
+
+def test_mg_vcycle_is_spd(gpu_available):
+    S, fs, w, rhs = _synthetic_system('t64')
+    rng = np.random.default_rng(5)
+    try:
+        _prepare(fs, w, np.ones(fs.n_data, bool))
+        nf = fs.n_full
+        kmask = np.zeros(nf, bool)
+        kmask[fs.keep_cols] = True
+        u = np.where(kmask, rng.standard_normal(nf), 0.0)
+        v = np.where(kmask, rng.standard_normal(nf), 0.0)
+        Vu, Vv = fs.solver.mg_apply(0, 1, u), fs.solver.mg_apply(0, 1, v)
+        Vu2 = fs.solver.mg_apply(0, 1, u)
+    finally:
+        fs.close()
+    assert np.array_equal(Vu, Vu2)                   # deterministic
+    assert np.all(Vu[~kmask] == 0.0)
+    a, b = v @ Vu, u @ Vv
+    assert abs(a - b) <= 1e-10 * (abs(a) + abs(b)), (a, b)
+    assert u @ Vu > 0 and v @ Vv > 0
+
+
+@pytest.mark.parametrize('name', ['sf3d', 'sf3d_edit', 'nb_xt'])
+def test_mg_pcg_matches_exact_solution(gpu_available, name):
+    g, fs, w, rhs = _golden_system(name)
+    try:
+        ok, why = fs.solver.cg_available(4)
+        if not ok:
+            pytest.skip(f'multigrid unavailable on {name}: {why}')
+        x = fs.solve(w, np.ones(fs.n_data, bool), rhs, precond=4, method=1, maxit=5000, **TOL)
+        st = fs.stats
+    finally:
+        fs.close()
+    xs = g['x']
+    assert st['method'] == 1 and st['istop'] in (1, 2), st
+    assert np.linalg.norm(x - xs) / np.linalg.norm(xs) <= REL
+    assert np.max(np.abs(x - xs)) <= ABS
+
+
+@pytest.mark.parametrize('which', ['t64', 't256'])
+def test_mg_pcg_iterations_and_solution(gpu_available, which):
+    """Same solution as block-Jacobi CGNR (and LSQR) in a fraction of the iterations; masked rows,
+    re-weighting and a warm start included."""
+    S, fs, w, rhs = _synthetic_system(which)
+    rng = np.random.default_rng(2)
+    keep = rng.random(fs.n_data) > 0.1
+    w2 = w * np.where(np.arange(w.size) < fs.n_data, rng.uniform(0.5, 2, w.size), 1.0)
+    try:
+        xb = fs.solve(w2, keep, rhs, precond=3, method=1, **TOL)
+        it_bj = fs.stats['iters']
+        xm = fs.solve(w2, keep, rhs, precond=4, method=1, **TOL)
+        st = dict(fs.stats)
+        xw = fs.solve(w2, keep, rhs, x0=xm * (1 + 1e-4), precond=4, method=1, **TOL)
+        it_warm = fs.stats['iters']
+    finally:
+        fs.close()
+    assert st['method'] == 1 and st['istop'] in (1, 2), st
+    assert np.linalg.norm(xm - xb) / np.linalg.norm(xb) <= 1e-8
+    assert np.linalg.norm(xw - xb) / np.linalg.norm(xb) <= 1e-8
+    assert st['iters'] * 5 <= it_bj, (st['iters'], it_bj)
+    assert it_warm <= st['iters']
+
+
+def test_mg_stiff(gpu_available):
+    """Stiff E_RMS (SURVEY.md §8(d) stress variant): the V-cycle stays a good preconditioner."""
+    S, fs, w, rhs = _synthetic_system(stiff=True)
+    keep = np.ones(fs.n_data, bool)
+    try:
+        xl = fs.solve(w, keep, rhs, precond=3, method=1, **TOL)
+        it_bj = fs.stats['iters']
+        xm = fs.solve(w, keep, rhs, precond=4, method=1, **TOL)
+        st = fs.stats
+    finally:
+        fs.close()
+    assert st['method'] == 1 and st['istop'] in (1, 2), st
+    assert np.linalg.norm(xm - xl) / np.linalg.norm(xl) <= 1e-7
+    assert st['iters'] * 3 <= it_bj, (st['iters'], it_bj)
+
+
+def test_mg_rejects_lsqr_and_unstructured(gpu_available):
+    from lssurf_amd._native import NativeError
+    S, fs, w, rhs = _synthetic_system('t64')
+    try:
+        with pytest.raises(NativeError):
+            fs.solve(w, np.ones(fs.n_data, bool), rhs, precond=4, method=0, **TOL)
+    finally:
+        fs.close()
