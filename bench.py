@@ -218,6 +218,8 @@ def main():
                     help='testing only: every rank on device 0 (RCCL over loopback sockets, distinct host ids)')
     ap.add_argument('--precond', type=int, default=3,
                     help='1: column scaling, 3: block-Jacobi per (y,x) node (smooth_fit default at this size)')
+    ap.add_argument('--solve-precond', default='auto', choices=['auto', '1', '3', '4'],
+                    help='preconditioner of the full solve: auto = multigrid (4) where it runs, else --precond')
     ap.add_argument('--method', default='cgnr', choices=['cgnr', 'lsqr'],
                     help='cgnr: PCG on the normal equations, fused normal-stencil operator (smooth_fit default); '
                          'lsqr: LSQR on the stencil operator')
@@ -308,16 +310,28 @@ def main():
 
     solve = {}
     if not args.no_solve:
-        # solve wall-time of the timed configuration (smooth_fit's default: CGNR + block-Jacobi),
-        # and LSQR with the same preconditioner for comparison
-        x, sst = solver.solve(rhs, op=args.op, precond=args.precond, method=meth)
-        solve = {'solve_time_s': sst['time_s'], 'solve_iters': int(sst['iters']), 'solve_istop': int(sst['istop']),
-                 'solve_method': ['lsqr', 'cgnr'][int(sst.get('method', 0))],
-                 'solve_precond': {1: 'column scaling', 3: 'block-Jacobi per (y,x) node'}.get(args.precond, args.precond)}
+        # solve wall-time with smooth_fit's default solver for this system: CGNR + the multigrid
+        # V-cycle (precond 4) where it runs (single GPU, per-node blocks), else the timed
+        # configuration; then CGNR + block-Jacobi and LSQR + block-Jacobi for comparison
+        names = {1: 'column scaling', 3: 'block-Jacobi per (y,x) node', 4: 'multigrid V-cycle (block-Jacobi smoothing)'}
+        sp = args.precond
+        if (args.solve_precond == 'auto' and meth == 1 and not isinstance(solver, _Dist) and args.precond == 3
+                and solver.cg_available(4)[0]) or args.solve_precond == '4':
+            sp = 4
+
+        def rec(st):
+            return {'solve_time_s': st['time_s'], 'solve_setup_s': st.get('setup_s', 0.0),
+                    'solve_iters': int(st['iters']), 'solve_istop': int(st['istop'])}
+        x, sst = solver.solve(rhs, op=args.op, precond=sp, method=meth)
+        solve = dict(rec(sst), solve_method=['lsqr', 'cgnr'][int(sst.get('method', 0))],
+                     solve_precond=names.get(sp, sp))
         if meth == 1 and not isinstance(solver, _Dist):   # distributed LSQR has no block-Jacobi
+            if sp == 4:
+                xb, sb = solver.solve(rhs, op=args.op, precond=3, method=1)
+                solve['solve_block_jacobi'] = rec(sb)
+                solve['solve_rel_diff_vs_block_jacobi'] = float(np.linalg.norm(x - xb) / np.linalg.norm(xb))
             xl, sl = solver.solve(rhs, op=args.op, precond=min(args.precond, 3), method=0)
-            solve['solve_lsqr'] = {'solve_time_s': sl['time_s'], 'solve_iters': int(sl['iters']),
-                                   'solve_istop': int(sl['istop'])}
+            solve['solve_lsqr'] = rec(sl)
             solve['solve_rel_diff_vs_lsqr'] = float(np.linalg.norm(x - xl) / np.linalg.norm(xl))
 
     cpu = None

@@ -80,7 +80,24 @@ class FitSystem:
             if blocks is not None:
                 self.solver.set_column_blocks_csr(*blocks)
                 self.has_blocks = True
+        self._mg = None            # multigrid (precond 4) availability, probed on first use
+        self.mg_build_s = 0.0
         self.stats = None
+
+    def multigrid_available(self, row_weight=None):
+        """True when the geometric multigrid preconditioner (lsq precond 4) runs on this system
+        (structured single-GPU smooth_fit system with per-node column blocks)."""
+        if self._mg is None:
+            if not self.has_blocks or self.formation != 'stencil':
+                self._mg = False
+            else:
+                if row_weight is not None and row_weight is not getattr(self, '_w_last', None):
+                    self.solver.set_row_weight(row_weight)
+                    self._w_last = row_weight
+                tic = time()
+                self._mg = bool(self.solver.cg_available(4)[0])   # builds the level hierarchy
+                self.mg_build_s = time() - tic
+        return self._mg
 
     def solve(self, row_weight, data_keep, rhs, x0=None, **opts):
         # re-upload only what changed between outer iterations (weights: same array object)
@@ -123,17 +140,18 @@ def print_TOC(G_data, Gc):
             print(f'\t{name}: {len(np.unique(rr)) / 1000}K')
 
 
-def _solve_opts(args, n, has_blocks=False):
+def _solve_opts(args, n, has_blocks=False, multigrid=False):
     """LSQR options.  precond 'auto': the exact dense-Cholesky preconditioner (R⁻¹ on the
-    device) when n <= lsq_dense_max, else block-Jacobi per (y, x) node when the system has node
-    blocks, else column scaling (maxit 50 n for the iterative ones)."""
+    device) when n <= lsq_dense_max, else the geometric multigrid V-cycle (precond 4, CGNR) when
+    the system supports it, else block-Jacobi per (y, x) node when the system has node blocks,
+    else column scaling (maxit 50 n for the iterative ones)."""
     pc_ = args['lsq_precond']
     if pc_ == 'auto':
-        pc_ = 2 if n <= args['lsq_dense_max'] else (3 if has_blocks else 1)
+        pc_ = 2 if n <= args['lsq_dense_max'] else (4 if multigrid else (3 if has_blocks else 1))
     maxit = args['lsq_maxit'] or (0 if pc_ == 2 else 50 * n)
     # method 'auto': CGNR (normal-stencil operator, column-space only) with the iterative
     # preconditioners — the library falls back to LSQR where the structured operator is absent
-    meth = {'auto': 1 if pc_ in (1, 3) else 0, 'lsqr': 0, 'cgnr': 1}[args.get('lsq_method', 'auto')]
+    meth = {'auto': 1 if pc_ in (1, 3, 4) else 0, 'lsqr': 0, 'cgnr': 1}[args.get('lsq_method', 'auto')]
     return dict(atol=args['lsq_atol'], btol=args['lsq_btol'], conlim=args['lsq_conlim'], maxit=maxit, precond=pc_,
                 method=meth)
 
@@ -163,13 +181,18 @@ def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grid
         tic = time()
         m0_last = m0
         x0 = x if (args['lsq_warm_start'] and x is not None) else None
-        x = system.solve(weight, in_TSE, rhs, x0=x0, **_solve_opts(args, system.keep_cols.size, system.has_blocks))
+        mg = args['lsq_precond'] == 'auto' and system.keep_cols.size > args['lsq_dense_max'] and \
+            system.multigrid_available(weight)
+        if mg and 'mg_build' not in timing:
+            timing['mg_build'] = system.mg_build_s
+        x = system.solve(weight, in_TSE, rhs, x0=x0, **_solve_opts(args, system.keep_cols.size, system.has_blocks, mg))
         if system.stats['istop'] == 7:
             print(f"smooth_fit: LSQR reached its iteration limit ({system.stats['iters']}) before the "
                   f"requested tolerance; raise lsq_maxit or use lsq_precond=2", flush=True)
         m0 = system.expand(x)
         timing['sparseqr_solve'] = time() - tic
         timing['lsq_iters'] += int(system.stats['iters'])
+        timing['lsq_setup'] = timing.get('lsq_setup', 0.) + float(system.stats.get('setup_s', 0.))
         timing['lsq_last'] = dict(system.stats)
         tic = time()
         r_data = data.z - system.data_forward(x)

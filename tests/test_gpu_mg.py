@@ -137,3 +137,18 @@ def test_mg_rejects_lsqr_and_unstructured(gpu_available):
             fs.solve(w, np.ones(fs.n_data, bool), rhs, precond=4, method=0, **TOL)
     finally:
         fs.close()
+
+
+def test_smooth_fit_multigrid_default(gpu_available):
+    """smooth_fit's 'auto' preconditioner picks the multigrid V-cycle above lsq_dense_max (forced
+    here with lsq_dense_max=0) and its outputs match the reference's golden fit."""
+    from conftest import golden_kwargs, golden_points
+    import lssurf_amd as LS
+    g = golden('sys_sf3d.npz')
+    out = LS.smooth_fit(data=golden_points(g), lsq_dense_max=0, **golden_kwargs(g))
+    assert out['timing']['lsq_last']['method'] == 1
+    for got, ref in ((out['m']['z0'].z0, g['z0']), (out['m']['dz'].dz, g['dz']), (out['data'].z_est, g['data_z_est'])):
+        ok = np.isfinite(ref)
+        assert np.linalg.norm(got[ok] - ref[ok]) / np.linalg.norm(ref[ok]) < 1e-6
+    assert np.nanmax(np.abs(out['m']['dz'].dz - g['dz'])) < ABS
+    assert np.array_equal(out['data'].three_sigma_edit, g['data_three_sigma_edit'])
