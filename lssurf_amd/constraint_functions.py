@@ -75,10 +75,13 @@ def setup_smoothness_constraints(grids, constraint_op_list, E_RMS, mask_scale, s
 
 
 def reference_epoch_keep_cols(n_cols, dz_grid, reference_epoch):
-    """Columns kept by Ip_c: every column except dz[:, :, reference_epoch] (ascending)."""
+    """Columns kept by Ip_c: every column except dz[:, :, reference_epoch] (ascending; the
+    np.setdiff1d of constraint_functions.py:112-151, as a boolean mask)."""
     iy, ix = np.meshgrid(np.arange(dz_grid.shape[0]), np.arange(dz_grid.shape[1]), indexing='ij')
     ref_cols = dz_grid.global_ind([iy.T.ravel(), ix.T.ravel(), np.full(iy.size, reference_epoch)])
-    return np.setdiff1d(np.arange(n_cols, dtype='int'), ref_cols)
+    keep = np.ones(int(n_cols), dtype=bool)
+    keep[ref_cols[(ref_cols >= 0) & (ref_cols < n_cols)]] = False
+    return np.flatnonzero(keep).astype('int')
 
 
 def build_reference_epoch_matrix(G_data, Gc, grids, reference_epoch, dz_mask=None):

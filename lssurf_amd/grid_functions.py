@@ -168,9 +168,15 @@ def validate_by_dz_mask(data, grids, valid_data):
         sampled = lin_op(tmp, name='interp_z').interp_mtx(data.coords()).toCSR().dot(
             dz.mask_3d.ravel().astype(float))
     else:
-        tmp = fd_grid(dz.bds[0:2], dz.delta[0:2])
-        sampled = lin_op(tmp, name='interp_z').interp_mtx(data.coords()[0:2]).toCSR().dot(
-            dz.mask.ravel().astype(float))
+        flat = np.ravel(dz.mask).astype(float)
+        if flat.size and np.all(flat == flat[0]) and np.isfinite(flat[0]) and flat[0] in (0.0, 1.0):
+            # uniform 0/1 mask: the bilinear weights sum to 1, so every point samples the mask
+            # value itself (the threshold below decides the same way without forming the operator)
+            pts = data.coords()[0:2]
+            sampled = np.full(np.size(pts[0]), flat[0])
+        else:
+            tmp = fd_grid(dz.bds[0:2], dz.delta[0:2])
+            sampled = lin_op(tmp, name='interp_z').interp_mtx(data.coords()[0:2]).toCSR().dot(flat)
     sampled[~np.isfinite(sampled)] = 0
     good = sampled > 0.5
     if np.any(~good):

@@ -56,6 +56,36 @@ def _grad2_dzdt_parts(g, DOF, t):
                                       [-t, -t, -t, -t, 0, 0, 0, 0]), cxy)]
 
 
+def _as_range(a):
+    """(first, last) when `a` is a contiguous ascending integer range, else None."""
+    a = np.asarray(a)
+    if a.ndim != 1 or a.size == 0 or a.dtype.kind not in 'iu':
+        return None
+    lo, hi = int(a[0]), int(a[-1])
+    if hi - lo + 1 != a.size:
+        return None
+    return (lo, hi) if np.array_equal(a, np.arange(lo, hi + 1, dtype=a.dtype)) else None
+
+
+def _union_sorted(arrays):
+    """np.unique(np.concatenate(arrays)) — computed from the index ranges when every array is a
+    contiguous range (the TOC column sets of grid operators), which avoids sorting ~10⁷ entries."""
+    if not arrays:
+        return np.array([], int)
+    ranges = [_as_range(a) for a in arrays]
+    if any(r is None for r in ranges):
+        return np.unique(np.concatenate(arrays))
+    ranges.sort()
+    merged = [list(ranges[0])]
+    for lo, hi in ranges[1:]:
+        if lo <= merged[-1][1] + 1:
+            merged[-1][1] = max(merged[-1][1], hi)
+        else:
+            merged.append([lo, hi])
+    dtype = np.result_type(*[np.asarray(a).dtype for a in arrays])
+    return np.concatenate([np.arange(lo, hi + 1, dtype=dtype) for lo, hi in merged])
+
+
 class lin_op:
     def __init__(self, grid=None, row_0=0, col_N=None, col_0=None, name=None):
         self.grid = grid
@@ -310,7 +340,7 @@ class lin_op:
                     TOC_cols[key] = cols
                     every.append(np.asarray(cols))
             if self.name is not None:
-                TOC_cols[self.name] = np.unique(np.concatenate(every)) if every else np.array([], int)
+                TOC_cols[self.name] = _union_sorted(every)
         if self.col_N is None:
             self.col_N = np.max(np.array([op.col_N for op in ops]))
         self.TOC['cols'] = TOC_cols

@@ -364,7 +364,7 @@ def smooth_fit(**kwargs):
     N_eq = G_data.N_eq + Gc.N_eq
     Ec = np.zeros(Gc.N_eq)
     for op in constraint_op_list:
-        Ec[Gc.TOC['rows'][op.name]] = op.expected
+        Ec[_as_slice(Gc.TOC['rows'][op.name])] = op.expected
     Ed = data.sigma.ravel()
     if np.any(Ed == 0):
         raise ValueError('zero value found in data sigma')
