@@ -158,6 +158,17 @@ int lsq_spmv(lsq_handle* h, int32_t trans, const double* x, double* y);
  * and :662, without moving the constraint rows over PCIe). */
 int lsq_spmv_rows(lsq_handle* h, int64_t first, int64_t count, const double* x, double* y);
 
+/* Output statistics of smooth_fit's parse_model (smooth_fit.py:318-347) without moving the
+ * operator to the host.  lsq_rows_sumsq: for each row range k, u = (G x) over rows
+ * [first[k], first[k] + count[k]) (x in compacted columns) and sum_w[k] = Σ (w_i u_i)², sum_u[k]
+ * = Σ u_i² with w the current row weights (R and RMS of each constraint type, smooth_fit.py:
+ * 324-331).  lsq_data_colsum: out = G_dataᵀ f over the FULL column space (length n_full; f has
+ * one value per data row, unweighted rows, removed columns included) — the per-node sums of the
+ * count / misfit maps (smooth_fit.py:341-347); structured systems on one (y, x) lattice only. */
+int lsq_rows_sumsq(lsq_handle* h, const double* x, int32_t n_ranges, const int64_t* first, const int64_t* count,
+                   double* sum_w, double* sum_u);
+int lsq_data_colsum(lsq_handle* h, const double* f, double* out);
+
 /* Bench / profiling hook: run exactly `iters` LSQR iterations on the current system (no early
  * stop), starting from the state left by the previous call (first call initialises from b).
  * Times only the device iterations. */

@@ -108,9 +108,13 @@ def node_column_blocks(grids, keep_cols, max_block=16):
         np.array_equal(a, b) for a, b in zip(z0.ctrs, dz.ctrs[:2]))
     parts = [(z0.col_0 + nodes)[:, None]] if same else []
     full = np.concatenate(parts + [dz_cols], axis=1)                           # (nodes, k)
-    pos = np.searchsorted(keep_cols, full)
-    pos_c = np.minimum(pos, keep_cols.size - 1)
-    kept = keep_cols[pos_c] == full
+    # compact position of every full column (a scatter, not a sorted search: keep_cols ascending)
+    n_full = int(max(full.max(), keep_cols.max() if keep_cols.size else 0)) + 1
+    where = np.full(n_full, -1, dtype=np.int64)
+    where[keep_cols] = np.arange(keep_cols.size)
+    pos = where[full]
+    kept = pos >= 0
+    pos_c = np.where(kept, pos, 0)
     cols, lens = [], []
     k_all = kept.sum(axis=1)
     if np.all(k_all == k_all[0]):                 # the usual case: same kept set at every node

@@ -14,6 +14,7 @@ int cg_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq_s
 int cg_iterate(System& S, const double* h_b, int64_t iters, const lsq_opts& o, lsq_stats* stats);
 void cg_profile(System& S, int reps, int precond, double* out);
 void cg_apply_normal(System& S, const double* h_p, double* h_q);
+void cg_data_colsum(System& S, const double* h_f, double* h_out);
 int lsqr_iterate(System& S, const double* h_b, int64_t iters, const lsq_opts& o, lsq_stats* stats);
 void lsqr_profile(System& S, int reps, int op, double* out);
 void lsqr_sigma_x(System& S, double* h_E);
@@ -562,6 +563,30 @@ int lsq_spmv_rows(lsq_handle* h, int64_t first, int64_t count, const double* x, 
         lsq::csr_spmv_rows(S, first, count, dx.p, dy.p);
         dy.download(y, count, S.stream);
         HIP_CHECK(hipStreamSynchronize(S.stream));
+        return 0;
+    });
+}
+
+int lsq_rows_sumsq(lsq_handle* h, const double* x, int32_t n_ranges, const int64_t* first, const int64_t* count,
+                   double* sum_w, double* sum_u) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_rows_sumsq: no matrix");
+        if (!x || n_ranges < 0 || (n_ranges && (!first || !count || !sum_w || !sum_u)))
+            return fail(S, "lsq_rows_sumsq: null argument");
+        for (int32_t k = 0; k < n_ranges; ++k)
+            if (first[k] < 0 || count[k] < 0 || first[k] + count[k] > S.G.m) return fail(S, "lsq_rows_sumsq: rows out of range");
+        lsq::DBuf<double> dx(std::max<int64_t>(S.G.n, 1));
+        dx.upload(x, S.G.n, S.stream);
+        for (int32_t k = 0; k < n_ranges; ++k) lsq::csr_rows_sumsq(S, dx.p, first[k], count[k], sum_w + k, sum_u + k);
+        return 0;
+    });
+}
+
+int lsq_data_colsum(lsq_handle* h, const double* f, double* out) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_data_colsum: no matrix");
+        if (!f || !out) return fail(S, "lsq_data_colsum: null argument");
+        lsq::cg_data_colsum(S, f, out);
         return 0;
     });
 }

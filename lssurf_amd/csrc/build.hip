@@ -375,6 +375,31 @@ __global__ __launch_bounds__(BLOCK) void k_csr_spmv(int64_t rows, const int64_t*
     }
 }
 
+// per-block partials of Σ (w_i u_i)² and Σ u_i² over rows [first, first + count), u = G x (the
+// row products in k_csr_spmv's order), w = the row weights (smooth_fit.py:324-331: R and RMS of
+// each constraint type)
+__global__ __launch_bounds__(BLOCK) void k_rows_sumsq(int64_t first, int64_t count, const int64_t* __restrict__ rp,
+                                                      const int32_t* __restrict__ ci, const double* __restrict__ val,
+                                                      const double* __restrict__ x, const double* __restrict__ w,
+                                                      double* __restrict__ pw, double* __restrict__ pu) {
+    double aw = 0.0, au = 0.0;
+    for (int64_t r = first + (int64_t)blockIdx.x * BLOCK + threadIdx.x; r < first + count; r += (int64_t)gridDim.x * BLOCK) {
+        double acc = 0.0;
+        for (int64_t e = rp[r]; e < rp[r + 1]; ++e) acc += val[e] * x[ci[e]];
+        const double rc = (w ? w[r] : 1.0) * acc;
+        aw += rc * rc;
+        au += acc * acc;
+    }
+    __shared__ double red[4];
+    const double sw = block_sum(aw, red);
+    __syncthreads();
+    const double su = block_sum(au, red);
+    if (threadIdx.x == 0) {
+        pw[blockIdx.x] = sw;
+        pu[blockIdx.x] = su;
+    }
+}
+
 // distributed layout: mark referenced columns; relabel columns to local ids and re-sort rows
 __global__ __launch_bounds__(BLOCK) void k_flag_cols(int64_t nnz, const int32_t* __restrict__ ci,
                                                      uint8_t* __restrict__ flags) {
@@ -776,6 +801,25 @@ void csr_spmv_rows(System& S, int64_t first, int64_t count, const double* dx, do
     hipLaunchKernelGGL(k_csr_spmv, dim3(grid_for(count)), dim3(BLOCK), 0, S.stream, count, S.G.rp.p + first, S.G.ci.p,
                        S.G.val.p, dx, dy);
     KERNEL_CHECK();
+}
+
+void csr_rows_sumsq(System& S, const double* dx, int64_t first, int64_t count, double* h_w, double* h_u) {
+    const int nb = grid_for(std::max<int64_t>(count, 1));
+    DBuf<double> pw(nb), pu(nb);
+    hipLaunchKernelGGL(k_rows_sumsq, dim3(nb), dim3(BLOCK), 0, S.stream, first, count, S.G.rp.p, S.G.ci.p, S.G.val.p, dx,
+                       S.roww.p, pw.p, pu.p);
+    KERNEL_CHECK();
+    std::vector<double> hw(nb), hu(nb);
+    pw.download(hw.data(), nb, S.stream);
+    pu.download(hu.data(), nb, S.stream);
+    HIP_CHECK(hipStreamSynchronize(S.stream));
+    double a = 0.0, b = 0.0;   // fixed order: deterministic
+    for (int i = 0; i < nb; ++i) {
+        a += hw[i];
+        b += hu[i];
+    }
+    *h_w = a;
+    *h_u = b;
 }
 
 void referenced_cols(System& S, uint8_t* h_flags) {

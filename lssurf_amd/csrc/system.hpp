@@ -355,6 +355,7 @@ void scaling_fill_values(System& S, int precond, bool set_csf = true);
 bool scaling_stale(const System& S, int precond);
 void csr_spmv(System& S, int trans, const double* dx, double* dy);  // unweighted G / Gᵀ products
 void csr_spmv_rows(System& S, int64_t first, int64_t count, const double* dx, double* dy);
+void csr_rows_sumsq(System& S, const double* dx, int64_t first, int64_t count, double* h_w, double* h_u);
 
 // block.hip
 void set_column_blocks(System& S, int64_t nb, const int64_t* ptr, const int32_t* cols);

@@ -72,6 +72,12 @@ def _union_sorted(arrays):
     contiguous range (the TOC column sets of grid operators), which avoids sorting ~10⁷ entries."""
     if not arrays:
         return np.array([], int)
+    seen, uniq = set(), []
+    for a in arrays:                     # the grid operators share their column array (_grid_cols)
+        if id(a) not in seen:
+            seen.add(id(a))
+            uniq.append(a)
+    arrays = uniq
     ranges = [_as_range(a) for a in arrays]
     if any(r is None for r in ranges):
         return np.unique(np.concatenate(arrays))
@@ -84,6 +90,16 @@ def _union_sorted(arrays):
             merged.append([lo, hi])
     dtype = np.result_type(*[np.asarray(a).dtype for a in arrays])
     return np.concatenate([np.arange(lo, hi + 1, dtype=dtype) for lo, hi in merged])
+
+
+def _grid_cols(g):
+    """The column range of grid g as one shared array per grid (TOC 'cols'; read-only use)."""
+    key = (g.col_0, g.N_nodes)
+    cached = getattr(g, '_toc_cols', None)
+    if cached is None or cached[0] != key:
+        cached = (key, np.arange(g.col_0, g.col_0 + g.N_nodes))
+        g._toc_cols = cached
+    return cached[1]
 
 
 class lin_op:
@@ -212,7 +228,7 @@ class lin_op:
             self.parts = None
         self.N_eq = n_eq
         self.TOC['rows'] = {self.name: np.arange(self.N_eq)}
-        self.TOC['cols'] = {g.name: np.arange(g.col_0, g.col_0 + g.N_nodes)}
+        self.TOC['cols'] = {g.name: _grid_cols(g)}
         self.__update_size_and_shape__()
         return self
 
@@ -298,7 +314,7 @@ class lin_op:
         self._lazy = build
         self.N_eq = npts
         self.TOC['rows'] = {self.name: np.arange(self.N_eq, dtype='int')}
-        self.TOC['cols'] = {g.name: np.arange(g.col_0, g.col_0 + g.N_nodes)}
+        self.TOC['cols'] = {g.name: _grid_cols(g)}
         self.parts = [dict(kind='interp', grid=g, pts=pts, rows=rows, row0=0, n_eq=npts)] \
             if xform is None and bounds_error else None
         self.__update_size_and_shape__()

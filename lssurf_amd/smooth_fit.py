@@ -220,7 +220,7 @@ def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grid
             if args['VERBOSE']:
                 print('Edited data empty, returning')
             return m0, sigma_extra, in_TSE, rs_data
-        if np.max(np.abs((m0_last - m0)[Gc.TOC['cols']['dz']])) < args['converge_tol_dz'] and \
+        if np.max(np.abs((m0_last - m0)[_as_slice(Gc.TOC['cols']['dz'])])) < args['converge_tol_dz'] and \
                 iteration > args['min_iterations']:
             if args['VERBOSE']:
                 print('Solution identical to previous iteration with tolerance %3.1f, exiting after iteration %d'
@@ -261,8 +261,29 @@ def _as_slice(idx):
     return idx
 
 
-def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args, ru=None):
-    """Output grids and fit statistics (smooth_fit.py:276-352)."""
+def _device_constraint_stats(system, m0, Gc, R, RMS):
+    """R and RMS of each constraint type (smooth_fit.py:318-331) reduced on the device from the
+    formed operator: no host copy of the 10⁷–10⁸ constraint residuals.  False when a type's rows
+    are not one contiguous range (then the caller takes the host path)."""
+    names, ranges = [], []
+    for eq_type in ['d2z_dt2', 'grad2_z0', 'grad2_dzdt', 'grad2_PS']:
+        if eq_type in Gc.TOC['rows']:
+            rows = _as_slice(Gc.TOC['rows'][eq_type])
+            if not isinstance(rows, slice):
+                return False
+            names.append(eq_type)
+            ranges.append((system.n_data + rows.start, rows.stop - rows.start))
+    if names:
+        sw, su = system.solver.rows_sumsq(m0[system.keep_cols], ranges)
+        for name, (first, count), a, b in zip(names, ranges, sw, su):
+            R[name] = a
+            RMS[name] = np.sqrt(b / count)
+    return True
+
+
+def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args, ru=None, system=None):
+    """Output grids and fit statistics (smooth_fit.py:276-352).  With the device `system` the
+    constraint statistics and the count / misfit maps are reduced on the device."""
     z0g, dzg = grids['z0'], grids['dz']
     m['z0'] = pc.grid.data().from_dict({'x': z0g.ctrs[1], 'y': z0g.ctrs[0], 'cell_area': z0g.cell_area,
                                         'mask': z0g.mask, 'z0': np.reshape(m0[G_data.TOC['cols']['z0']], z0g.shape)})
@@ -277,33 +298,46 @@ def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args,
     m['extent'] = np.concatenate((z0g.bds[1], z0g.bds[0]))
     m['sensor_bias_grids'] = {}
     m['jitter_bias_grids'] = {}
-    if ru is None:               # unscaled constraint residuals Gc·m0 (device product when available)
-        ru = Gc.toCSR().dot(m0)
-    for eq_type in ['d2z_dt2', 'grad2_z0', 'grad2_dzdt', 'grad2_PS']:
-        if eq_type in Gc.TOC['rows']:
-            rows = _as_slice(Gc.TOC['rows'][eq_type])
-            rc = (1. / Ec[rows]) * ru[rows]   # TCinv_cov.dot(ru), smooth_fit.py:324-326
-            R[eq_type] = np.sum(rc ** 2)
-            RMS[eq_type] = np.sqrt(np.mean(ru[rows] ** 2))
+    if system is None or not _device_constraint_stats(system, m0, Gc, R, RMS):
+        if ru is None:           # unscaled constraint residuals Gc·m0 (device product when available)
+            ru = system.solver.spmv(m0[system.keep_cols])[system.n_data:] if system is not None else Gc.toCSR().dot(m0)
+        for eq_type in ['d2z_dt2', 'grad2_z0', 'grad2_dzdt', 'grad2_PS']:
+            if eq_type in Gc.TOC['rows']:
+                rows = _as_slice(Gc.TOC['rows'][eq_type])
+                rc = (1. / Ec[rows]) * ru[rows]   # TCinv_cov.dot(ru), smooth_fit.py:324-326
+                R[eq_type] = np.sum(rc ** 2)
+                RMS[eq_type] = np.sqrt(np.mean(ru[rows] ** 2))
     tse = data.three_sigma_edit
     r = (data.z - data.z_est)[tse]
     if args['sigma_extra_relax']:
         r_scaled = r / np.sqrt(data.sigma[tse] ** 2 + data.sigma_extra[tse] ** 2)
     else:
         r_scaled = r / data.sigma[tse]
-    # Gselᵀ·{1, r_scaled², r²} of smooth_fit.py:341-347 as weighted column sums of G_data's
-    # triplets over the kept data rows (no host CSR of the 24 M-entry data operator)
-    rr, cc, vv = G_data.triplets()
+    # Gselᵀ·{1, r_scaled², r²} of smooth_fit.py:341-347: weighted column sums over the kept data rows
     tse_b = np.asarray(tse).astype(bool).ravel()
-    rows_tse = np.flatnonzero(tse_b)
-    pos = np.full(tse_b.shape, -1)
-    pos[rows_tse] = np.arange(rows_tse.size)
-    sel = tse_b[rr] & (vv != 0)
-    c_sel, v_sel, p_sel = cc[sel], vv[sel], pos[rr[sel]]
     n_cols = G_data.col_N
-    sums = {'count': np.bincount(c_sel, weights=v_sel, minlength=n_cols),
-            'scaled': np.bincount(c_sel, weights=v_sel * (r_scaled ** 2)[p_sel], minlength=n_cols),
-            'plain': np.bincount(c_sel, weights=v_sel * (r ** 2)[p_sel], minlength=n_cols)}
+    sums = None
+    if system is not None and getattr(system, 'formation', None) == 'stencil':
+        from ._native import NativeError
+        fs = {'count': tse_b.astype(float)}
+        for key, vals in (('scaled', r_scaled ** 2), ('plain', r ** 2)):
+            f = np.zeros(tse_b.size)
+            f[tse_b] = vals
+            fs[key] = f
+        try:   # node gather over the points sorted by cell (no host triplets of the data operator)
+            sums = {k: system.solver.data_colsum(f)[:n_cols] for k, f in fs.items()}
+        except NativeError:
+            sums = None
+    if sums is None:   # host: weighted column sums of G_data's triplets
+        rr, cc, vv = G_data.triplets()
+        rows_tse = np.flatnonzero(tse_b)
+        pos = np.full(tse_b.shape, -1)
+        pos[rows_tse] = np.arange(rows_tse.size)
+        sel = tse_b[rr] & (vv != 0)
+        c_sel, v_sel, p_sel = cc[sel], vv[sel], pos[rr[sel]]
+        sums = {'count': np.bincount(c_sel, weights=v_sel, minlength=n_cols),
+                'scaled': np.bincount(c_sel, weights=v_sel * (r_scaled ** 2)[p_sel], minlength=n_cols),
+                'plain': np.bincount(c_sel, weights=v_sel * (r ** 2)[p_sel], minlength=n_cols)}
     for ff in ['dz', 'z0']:
         cols = G_data.TOC['cols'][ff]
         m[ff].assign({'count': sums['count'][cols].reshape(grids[ff].shape)})
@@ -406,8 +440,7 @@ def smooth_fit(**kwargs):
             averaging_ops = setup_averaging_ops(grids['dz'], grids['dz'].col_N, args, grids['dz'].cell_area)
             averaging_ops.update(setup_z0_avg(grids, grids['dz'].col_N, args))
             averaging_ops.update(setup_avg_mask_ops(grids['dz'], G_data.col_N, args['avg_masks'], args['dzdt_lags']))
-            ru = system.solver.spmv(m0[keep_cols])[system.n_data:]
-            parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args, ru=ru)
+            parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args, system=system)
             tse = data.three_sigma_edit == 1
             r_data = data.z_est[tse] - data.z[tse]
             R['data'] = np.sum((r_data / data.sigma[tse]) ** 2)

@@ -234,6 +234,23 @@ class LSQSolver:
         return y
 
 
+    def rows_sumsq(self, x, ranges):
+        """For each (first, count) row range: (Σ (w_i (G x)_i)², Σ (G x)_i²), w = row weights."""
+        x = as_c(x, np.float64)
+        f = as_c([r[0] for r in ranges], np.int64)
+        c = as_c([r[1] for r in ranges], np.int64)
+        sw, su = np.zeros(len(ranges)), np.zeros(len(ranges))
+        self._check(self._L.lsq_rows_sumsq(self._h, ptr(x), len(ranges), ptr(f), ptr(c), ptr(sw), ptr(su)),
+                    'lsq_rows_sumsq')
+        return sw, su
+
+    def data_colsum(self, f):
+        """G_dataᵀ f over the full column space (unweighted data rows; f per data row)."""
+        f = as_c(f, np.float64)
+        out = np.zeros(self.n_full)
+        self._check(self._L.lsq_data_colsum(self._h, ptr(f), ptr(out)), 'lsq_data_colsum')
+        return out
+
     def spmv_rows(self, x, first, count):
         """Rows [first, first + count) of G x (unweighted)."""
         x = as_c(x, np.float64)
