@@ -180,6 +180,18 @@ int lsq_iterate(lsq_handle* h, const double* b, int64_t iters, const lsq_opts* o
  * lsq_get_rinv: R^-1 as a dense n x n row-major upper-triangular matrix. */
 int lsq_sigma_x(lsq_handle* h, double* E);
 int lsq_get_rinv(lsq_handle* h, double* Rinv);
+/* Error propagation without a dense factor (replaces sparseqr.rz + inv_tr_upper +
+ * propagate_qz_errors at smooth_fit.py:218-253 and op.grid_error(Ip_c·Rinv) at :266-270).
+ * perm (length n, nullable = identity): new position j -> compact column perm[j]; an order in
+ * which AᵀA is banded (smooth_fit: node-major).  AᵀA of the current weighted, masked system is
+ * equilibrated and factored inside its band (64×64 tiles, f64 MFMA); the rows of R⁻¹ needed are
+ * formed by banded forward sweeps (never stored).  E[c] = sqrt(((AᵀA)⁻¹)_cc) per compact column.
+ * For the n_ops rows of the CSR op (op_ptr[n_ops+1], op_col = compact columns, op_val):
+ * op_err[i] = sqrt(op_i (AᵀA)⁻¹ op_iᵀ).  info (nullable, 4): band width in 64-column tiles, tile
+ * rows, device bytes, 64×64 tile products of the sweeps.  Error -2 when the band does not fit the
+ * device's free memory. */
+int lsq_cov_band(lsq_handle* h, const int32_t* perm, double* E, int64_t n_ops, const int64_t* op_ptr,
+                 const int32_t* op_col, const double* op_val, double* op_err, int64_t* info);
 
 /* ---- multi-GPU (one process per GPU) --------------------------------------
  * lsq_dist_unique_id: rank 0 creates the 128-byte RCCL id; the caller broadcasts it (any

@@ -12,7 +12,7 @@ CSRC = os.path.join(HERE, 'csrc')
 OBJ = os.path.join(CSRC, 'build')
 LIB = os.path.join(HERE, 'liblsqsurf.so')
 ARCH = 'gfx950'
-SOURCES = ['scan.hip', 'build.hip', 'assemble.hip', 'lsqr.hip', 'dense.hip', 'block.hip', 'api.hip', 'tri.hip', 'rde.hip']
+SOURCES = ['scan.hip', 'build.hip', 'assemble.hip', 'lsqr.hip', 'dense.hip', 'band.hip', 'block.hip', 'api.hip', 'tri.hip', 'rde.hip']
 # bit-exact recurrences (triangular kernels, formation) must not be FMA-contracted
 NO_CONTRACT = {'tri.hip', 'build.hip', 'assemble.hip', 'rde.hip'}
 COMMON = ['-O3', '-std=c++17', '-fPIC', f'--offload-arch={ARCH}', '-Wall', '-Wno-unused-function',

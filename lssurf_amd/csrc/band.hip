@@ -1,0 +1,544 @@
+// band.hip — error propagation (smooth_fit compute_E, smooth_fit.py:212-274) without a dense
+// factor.
+//
+// The reference factors A = Q R E' with SuiteSparseQR (`sparseqr.rz`, :218), inverts R column by
+// column with the Cython `inv_tr_upper` (|x| > 1e-5 kept, :240-248) and reports
+// E0 = sqrt(row sums of R⁻¹²) = sqrt(diag((AᵀA)⁻¹)) (:253) and, for every averaging operator,
+// sqrt(row sums of (op·R⁻¹)²) = sqrt(diag(op (AᵀA)⁻¹ opᵀ)) (:266-270).  With the columns ordered
+// so that AᵀA is banded — smooth_fit's columns node-major ((y, x) rows of nodes, each node's z0 and
+// kept dz epochs together): a band of ~2 node rows — the factor is banded too:
+//
+//   N = AᵀA           in the caller's column order, stored as a band of 64×64 tiles (tile row I
+//                     keeps tiles I..I+w, w from the row pattern of A), upper triangle, then
+//                     equilibrated (S N S, S = diag(N)^-1/2)
+//   N = RᵀR           right-looking tile Cholesky inside the band: per tile column K, POTRF of
+//                     the diagonal tile (+ D_K = R_KK⁻¹), TRSM of the tile row by substitution,
+//                     SYRK/GEMM of the trailing triangle on f64 MFMA
+//   rows of R⁻¹       y = R⁻ᵀ e_j by banded forward sweeps, 64 right-hand sides per workgroup,
+//                     Y_K = D_Kᵀ (O_K − Σ_{I=K−w}^{K−1} R_IKᵀ Y_I), only the last w+1 tiles of y
+//                     live (a ring per workgroup); E_j² = ‖y‖²; op rows the same way with o = op_i
+//
+// Cost ~T²(w+1)/2 tile products (T = n/64) against the dense path's 2n³/3 flops (dense.hip), the
+// same accuracy class as the dense R⁻¹ (measured 1e-13 relative to LAPACK at 48²×12), band
+// storage n·(w+1)·64 doubles.  Takahashi's recurrence for the band of (AᵀA)⁻¹ costs only
+// ~T(w+1)² but its sums cancel in proportion to cond(AᵀA): measured 3e-6 relative at 48²×12,
+// 2 % at 64²×12 and negative diagonals beyond — so it is not used.
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <stdexcept>
+#include <vector>
+
+#include "system.hpp"
+
+namespace lsq {
+namespace {
+
+constexpr int TB = 64;
+constexpr int64_t TT = (int64_t)TB * TB;
+constexpr int LDP = TB + 1;   // LDS tile pitch
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+struct BandDev {
+    int64_t T;    // tile rows (n padded to T·64)
+    int w;        // tiles right of the diagonal kept per tile row
+    double* R;    // Cholesky factor band
+    double* D;    // R_KK⁻¹ per tile row
+};
+
+__device__ __forceinline__ double* btile(double* base, int w, int64_t I, int64_t J) {
+    return base + ((I * (w + 1)) + (J - I)) * TT;
+}
+
+// LDS image of a row-major 64×64 tile (TR: transposed)
+template <bool TR>
+__device__ __forceinline__ void lds_tile(double* S, const double* __restrict__ src) {
+    for (int idx = threadIdx.x; idx < TT; idx += BLOCK) {
+        const int r = idx >> 6, c = idx & 63;
+        const double v = src[idx];
+        if (TR) S[c * LDP + r] = v;
+        else S[r * LDP + c] = v;
+    }
+}
+
+// acc += op(A)·B over one 64-deep tile pair held in LDS (A [i][k], or [k][i] when AT; B [k][j]);
+// wave wv owns the 32×32 output block (r0, c0) as 2×2 f64 16×16x4 MFMA accumulators: element
+// (s, t, reg) is row r0 + 16s + (lane>>4) + 4·reg, column c0 + 16t + (lane&15)
+template <bool AT = false>
+__device__ __forceinline__ void mma_tile(const double* A, const double* B, d4 (&acc)[2][2]) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int r0 = (wv >> 1) * 32, c0 = (wv & 1) * 32;
+    const int li = lane & 15, lk = lane >> 4;
+#pragma unroll 4
+    for (int k0 = 0; k0 < TB; k0 += 4) {
+        const int k = k0 + lk;
+        const double a0 = AT ? A[k * LDP + r0 + li] : A[(r0 + li) * LDP + k];
+        const double a1 = AT ? A[k * LDP + r0 + 16 + li] : A[(r0 + 16 + li) * LDP + k];
+        const double b0 = B[k * LDP + c0 + li], b1 = B[k * LDP + c0 + 16 + li];
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+}
+
+// a tile pair in registers (16-byte loads, 8 per thread per tile) and from there into LDS, so
+// the next pair's loads are in flight while the MFMAs of the current one run
+struct TilePair {
+    double2 a[TT / 2 / BLOCK], b[TT / 2 / BLOCK];
+    __device__ __forceinline__ void load(const double* __restrict__ pa, const double* __restrict__ pb) {
+        const double2* a2 = reinterpret_cast<const double2*>(pa);
+        const double2* b2 = reinterpret_cast<const double2*>(pb);
+#pragma unroll
+        for (int i = 0; i < TT / 2 / BLOCK; ++i) {
+            a[i] = a2[threadIdx.x + BLOCK * i];
+            b[i] = b2[threadIdx.x + BLOCK * i];
+        }
+    }
+    __device__ __forceinline__ void store(double* SA, double* SB) const {
+#pragma unroll
+        for (int i = 0; i < TT / 2 / BLOCK; ++i) {
+            const int idx = 2 * (threadIdx.x + BLOCK * i), r = idx >> 6, c = idx & 63;
+            SA[r * LDP + c] = a[i].x;
+            SA[r * LDP + c + 1] = a[i].y;
+            SB[r * LDP + c] = b[i].x;
+            SB[r * LDP + c + 1] = b[i].y;
+        }
+    }
+};
+
+__device__ __forceinline__ void acc_zero(d4 (&acc)[2][2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) acc[s][t] = d4{0.0, 0.0, 0.0, 0.0};
+}
+
+// visit every accumulator element: f(row, col, value&)
+template <class F>
+__device__ __forceinline__ void acc_each(d4 (&acc)[2][2], F&& f) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int r0 = (wv >> 1) * 32, c0 = (wv & 1) * 32;
+    const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) f(r0 + 16 * s + lk + 4 * g, c0 + 16 * t + li, acc[s][t][g]);
+}
+
+// tile row span of the rows of A (masked rows excluded): w = max over rows of (last − first tile)
+__global__ __launch_bounds__(BLOCK) void k_band_width(int64_t m, const int64_t* __restrict__ rp,
+                                                      const int32_t* __restrict__ ci, const int32_t* __restrict__ pinv,
+                                                      const double* __restrict__ rs, int* __restrict__ wmax) {
+    int local = 0;
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += (int64_t)gridDim.x * BLOCK) {
+        if (rs[i] == 0.0) continue;
+        int lo = INT_MAX, hi = -1;
+        for (int64_t f = rp[i]; f < rp[i + 1]; ++f) {
+            const int t = pinv[ci[f]] >> 6;
+            lo = min(lo, t);
+            hi = max(hi, t);
+        }
+        if (hi >= 0) local = max(local, hi - lo);
+    }
+    for (int o = 32; o > 0; o >>= 1) local = max(local, __shfl_xor(local, o));
+    if ((threadIdx.x & 63) == 0 && local > 0) atomicMax(wmax, local);
+}
+
+// N = AᵀA in the new order, upper band: one thread owns row j of N (new column j = old perm[j]),
+// contributions in the order of dense.hip's k_normal_rows (so every entry is the same sum)
+__global__ __launch_bounds__(BLOCK) void k_band_normal(int64_t n, int64_t npad, BandDev b,
+                                                       const int32_t* __restrict__ perm,
+                                                       const int32_t* __restrict__ pinv,
+                                                       const int64_t* __restrict__ trp, const int32_t* __restrict__ tci,
+                                                       const double* __restrict__ tval, const int64_t* __restrict__ rp,
+                                                       const int32_t* __restrict__ ci, const double* __restrict__ val,
+                                                       const double* __restrict__ rs) {
+    for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < npad; j += (int64_t)gridDim.x * BLOCK) {
+        const int64_t I = j >> 6;
+        const int rj = (int)(j & 63);
+        if (j >= n) {
+            btile(b.R, b.w, I, I)[rj * TB + rj] = 1.0;
+            continue;
+        }
+        const int32_t jo = perm[j];
+        for (int64_t e = trp[jo]; e < trp[jo + 1]; ++e) {
+            const int32_t i = tci[e];
+            const double a = tval[e] * rs[i];
+            if (a == 0.0) continue;
+            for (int64_t f = rp[i]; f < rp[i + 1]; ++f) {
+                const int64_t k = pinv[ci[f]];
+                if (k < j) continue;
+                btile(b.R, b.w, I, k >> 6)[rj * TB + (k & 63)] += a * (val[f] * rs[i]);
+            }
+        }
+    }
+}
+
+// symmetric diagonal scaling Ñ = S N S, S = diag(N)^(-1/2) (z0 and dz columns differ in scale by
+// orders of magnitude; the factor of Ñ is better balanced)
+__global__ __launch_bounds__(BLOCK) void k_band_dscale(BandDev b, int64_t npad, double* __restrict__ sc) {
+    for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < npad; j += (int64_t)gridDim.x * BLOCK) {
+        const int r = (int)(j & 63);
+        const double d = btile(b.R, b.w, j >> 6, j >> 6)[r * TB + r];
+        sc[j] = d > 0.0 ? 1.0 / sqrt(d) : 1.0;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_band_apply_scale(BandDev b, const double* __restrict__ sc) {
+    const int64_t ntile = b.T * (b.w + 1);
+    for (int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x; e < ntile * TT; e += (int64_t)gridDim.x * BLOCK) {
+        const int64_t tix = e / TT;
+        const int64_t I = tix / (b.w + 1), J = I + tix % (b.w + 1);
+        if (J >= b.T) continue;
+        const int idx = (int)(e - tix * TT);
+        b.R[e] *= sc[I * TB + (idx >> 6)] * sc[J * TB + (idx & 63)];
+    }
+}
+
+// POTRF of tile (K, K) in LDS (as dense.hip's k_potrf_diag), then D_K = R_KK⁻¹ (column-parallel
+// back substitution); the lower triangle of R_KK is zeroed
+__global__ __launch_bounds__(BLOCK) void k_band_potrf(BandDev b, int64_t K, int* err) {
+    __shared__ double A[TB * LDP];
+    __shared__ double X[TB * LDP];
+    double* Rt = btile(b.R, b.w, K, K);
+    for (int idx = threadIdx.x; idx < TT; idx += BLOCK) {
+        const int r = idx >> 6, c = idx & 63;
+        A[r * LDP + c] = c >= r ? Rt[idx] : 0.0;
+        X[r * LDP + c] = 0.0;
+    }
+    __syncthreads();
+    for (int j = 0; j < TB; ++j) {
+        if (threadIdx.x == 0) {
+            const double d = A[j * LDP + j];
+            if (!(d > 0.0)) {
+                atomicExch(err, 1);
+                A[j * LDP + j] = 1.0;
+            } else {
+                A[j * LDP + j] = sqrt(d);
+            }
+        }
+        __syncthreads();
+        const double piv = A[j * LDP + j];
+        for (int k = j + 1 + threadIdx.x; k < TB; k += BLOCK) A[j * LDP + k] /= piv;
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < TT; idx += BLOCK) {
+            const int i = idx >> 6, k = idx & 63;
+            if (i > j && k >= i) A[i * LDP + k] -= A[j * LDP + i] * A[j * LDP + k];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < TB) {
+        const int c = threadIdx.x;
+        for (int i = c; i >= 0; --i) {
+            double x = (i == c) ? 1.0 : 0.0;
+            for (int j = i + 1; j <= c; ++j) x -= A[i * LDP + j] * X[j * LDP + c];
+            X[i * LDP + c] = x / A[i * LDP + i];
+        }
+    }
+    __syncthreads();
+    double* Dk = b.D + K * TT;
+    for (int idx = threadIdx.x; idx < TT; idx += BLOCK) {
+        const int r = idx >> 6, c = idx & 63;
+        Rt[idx] = A[r * LDP + c];
+        Dk[idx] = X[r * LDP + c];
+    }
+}
+
+// R_KJ = R_KK⁻ᵀ N_KJ for J = K+1..K+m (one workgroup per tile), by forward substitution as
+// dense.hip's k_trsm_panel: multiplying by the explicit D_Kᵀ instead loses ~cond(R_KK)·ε per tile
+// row and compounds over the factor (measured 1e-6 on E at 48²×12 against 3e-13 here)
+__global__ __launch_bounds__(BLOCK) void k_band_trsm(BandDev b, int64_t K) {
+    __shared__ double R[TB * LDP];
+    __shared__ double X[TB * LDP];
+    double* Nt = btile(b.R, b.w, K, K + 1 + blockIdx.x);
+    lds_tile<false>(R, btile(b.R, b.w, K, K));
+    lds_tile<false>(X, Nt);
+    __syncthreads();
+    for (int i = 0; i < TB; ++i) {
+        const double piv = R[i * LDP + i];
+        if (threadIdx.x < TB) X[i * LDP + threadIdx.x] /= piv;
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < TT; idx += BLOCK) {
+            const int p = idx >> 6, c = idx & 63;
+            if (p > i) X[p * LDP + c] -= R[i * LDP + p] * X[i * LDP + c];
+        }
+        __syncthreads();
+    }
+    for (int idx = threadIdx.x; idx < TT; idx += BLOCK) Nt[idx] = X[(idx >> 6) * LDP + (idx & 63)];
+}
+
+// N_{K+a, K+c} −= R_{K,K+a}ᵀ R_{K,K+c}, 1 ≤ a ≤ c ≤ m (grid m·m, lower pairs idle)
+__global__ __launch_bounds__(BLOCK) void k_band_syrk(BandDev b, int64_t K, int m) {
+    const int a = blockIdx.x % m + 1, c = blockIdx.x / m + 1;
+    if (a > c) return;
+    __shared__ double A[TB * LDP];
+    __shared__ double B[TB * LDP];
+    lds_tile<true>(A, btile(b.R, b.w, K, K + a));
+    lds_tile<false>(B, btile(b.R, b.w, K, K + c));
+    __syncthreads();
+    d4 acc[2][2];
+    acc_zero(acc);
+    mma_tile(A, B, acc);
+    double* Ct = btile(b.R, b.w, K + a, K + c);
+    acc_each(acc, [&](int r, int cc, double v) { Ct[r * TB + cc] -= v; });
+}
+
+// y = R⁻ᵀ o for the 64 right-hand sides of one workgroup, tile row by tile row from the first
+// non-zero row K0: Y_K = D_Kᵀ (O_K − Σ_{I=max(K0,K−w)}^{K−1} R_IKᵀ Y_I); out = ‖y‖² per right-hand
+// side.  Only the last w+1 tiles of y are live: a ring per workgroup (the __threadfence closing
+// each step also invalidates this CU's L1, so a rewritten slot is read fresh).
+// IDENT: o = e_{64J..64J+63}, J = j0 + blockIdx.x (the diagonal of N⁻¹).  Otherwise op rows: the
+// workgroup's segments [sp[rt], sp[rt+1]) each hold one tile row segK[s] and the entries
+// [segE[s], segE[s+1]) as (row-in-tile << 6 | rhs) in el and the value in ev (× s_j here).
+template <bool IDENT>
+__global__ __launch_bounds__(BLOCK) void k_band_sweep(BandDev b, int64_t j0, const int64_t* __restrict__ sp,
+                                                      const int64_t* __restrict__ segK,
+                                                      const int64_t* __restrict__ segE, const int32_t* __restrict__ el,
+                                                      const double* __restrict__ ev, const double* __restrict__ sc,
+                                                      double* __restrict__ ring, double* __restrict__ out) {
+    __shared__ double A[TB * LDP];
+    __shared__ double B[TB * LDP];
+    __shared__ double red[4][4][2][16];
+    const int64_t rt = blockIdx.x;
+    const int64_t W1 = b.w + 1;
+    double* Rg = ring + rt * W1 * TT;
+    int64_t s = 0, s1 = 0, K0 = 0;
+    if (IDENT) {
+        K0 = j0 + rt;
+    } else {
+        s = sp[rt];
+        s1 = sp[rt + 1];
+        K0 = segK[s];
+    }
+    double ss[2] = {0.0, 0.0};
+    TilePair tp;
+    for (int64_t K = K0; K < b.T; ++K) {
+        d4 acc[2][2];
+        acc_zero(acc);
+        const int64_t I0 = max<int64_t>(K0, K - b.w);
+        if (I0 < K) tp.load(btile(b.R, b.w, I0, K), Rg + (I0 % W1) * TT);
+        for (int64_t I = I0; I < K; ++I) {
+            __syncthreads();
+            tp.store(A, B);
+            __syncthreads();
+            if (I + 1 < K) tp.load(btile(b.R, b.w, I + 1, K), Rg + ((I + 1) % W1) * TT);
+            mma_tile<true>(A, B, acc);
+        }
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < TT; idx += BLOCK) {
+            const int r = idx >> 6, c = idx & 63;
+            B[r * LDP + c] = (IDENT && K == K0 && r == c) ? 1.0 : 0.0;
+            A[r * LDP + c] = b.D[K * TT + idx];
+        }
+        if (!IDENT && s < s1 && segK[s] == K) {
+            __syncthreads();
+            for (int64_t e = segE[s] + threadIdx.x; e < segE[s + 1]; e += BLOCK) {
+                const int p = el[e];
+                B[(p >> 6) * LDP + (p & 63)] = ev[e] * sc[K * TB + (p >> 6)];
+            }
+            ++s;
+        }
+        __syncthreads();
+        acc_each(acc, [&](int r, int c, double v) { B[r * LDP + c] -= v; });
+        __syncthreads();
+        acc_zero(acc);
+        mma_tile<true>(A, B, acc);   // D_Kᵀ · X
+        double* Yk = Rg + (K % W1) * TT;
+        acc_each(acc, [&](int r, int c, double v) {
+            Yk[r * TB + c] = v;
+            ss[((c & 31) >= 16) ? 1 : 0] += v * v;
+        });
+        __threadfence();
+    }
+    // column sums: thread (wave wv, lane) holds columns c0 + 16t + (lane&15) over rows lk + 4g (+16s)
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    red[wv][lane >> 4][0][lane & 15] = ss[0];
+    red[wv][lane >> 4][1][lane & 15] = ss[1];
+    __syncthreads();
+    if (threadIdx.x < TB) {
+        const int c = threadIdx.x;
+        const int half = c >> 5, t = (c & 31) >> 4, li = c & 15;
+        double sum = 0.0;
+        for (int wr = 0; wr < 2; ++wr)
+            for (int lk = 0; lk < 4; ++lk) sum += red[wr * 2 + half][lk][t][li];
+        out[((IDENT ? j0 : 0) + rt) * TB + c] = sum;
+    }
+}
+
+// E[perm[j]] = sqrt(ss_j)·s_j from the identity sweeps
+__global__ __launch_bounds__(BLOCK) void k_band_diag_sweep(int64_t n, const int32_t* __restrict__ perm,
+                                                           const double* __restrict__ ssq,
+                                                           const double* __restrict__ sc, double* __restrict__ E) {
+    for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLOCK)
+        E[perm[j]] = sqrt(ssq[j]) * sc[j];
+}
+
+}  // namespace
+
+namespace {
+
+// op rows (new column order) as sweep right-hand sides: 64 rows per workgroup, entries grouped by
+// tile row (segments), each workgroup starting at its first non-zero tile row
+struct SweepOps {
+    std::vector<int64_t> sp{0}, segK, segE{0};
+    std::vector<int32_t> el;
+    std::vector<double> ev;
+    int64_t gemms = 0;
+};
+
+SweepOps sweep_ops(const std::vector<int64_t>& rows, const int64_t* rp, const int32_t* ci, const double* v,
+                   const std::vector<int32_t>& pinv, int64_t T, int w) {
+    SweepOps o;
+    struct Ent { int64_t K; int32_t p; double v; };
+    for (size_t r0 = 0; r0 < rows.size(); r0 += TB) {
+        std::vector<Ent> ents;
+        for (size_t q = r0; q < std::min(rows.size(), r0 + TB); ++q)
+            for (int64_t e = rp[rows[q]]; e < rp[rows[q] + 1]; ++e) {
+                const int64_t j = pinv[ci[e]];
+                ents.push_back({j >> 6, (int32_t)(((j & 63) << 6) | (int64_t)(q - r0)), v[e]});
+            }
+        std::stable_sort(ents.begin(), ents.end(), [](const Ent& a, const Ent& b) { return a.K < b.K; });
+        if (ents.empty()) ents.push_back({T - 1, 0, 0.0});   // an all-zero row block: one trivial step
+        for (size_t e = 0; e < ents.size(); ++e) {
+            if (e == 0 || ents[e].K != ents[e - 1].K) {
+                if (e) o.segE.push_back((int64_t)o.el.size());
+                o.segK.push_back(ents[e].K);
+            }
+            o.el.push_back(ents[e].p);
+            o.ev.push_back(ents[e].v);
+        }
+        o.segE.push_back((int64_t)o.el.size());
+        o.sp.push_back((int64_t)o.segK.size());
+        o.gemms += (T - ents.front().K) * (int64_t)(w + 1);
+    }
+    return o;
+}
+
+// launch the sweeps of `nwg` workgroups in batches whose rings fit `ring` (cap workgroups each)
+template <bool IDENT>
+void run_sweeps(hipStream_t st, const BandDev& b, int64_t nwg, int64_t cap, const int64_t* sp, const int64_t* segK,
+                const int64_t* segE, const int32_t* el, const double* ev, const double* sc, double* ring, double* out) {
+    for (int64_t g0 = 0; g0 < nwg; g0 += cap) {
+        const int64_t g = std::min(cap, nwg - g0);
+        if (IDENT)
+            hipLaunchKernelGGL(k_band_sweep<true>, dim3((unsigned)g), dim3(BLOCK), 0, st, b, g0, sp, segK, segE, el, ev,
+                               sc, ring, out);
+        else
+            hipLaunchKernelGGL(k_band_sweep<false>, dim3((unsigned)g), dim3(BLOCK), 0, st, b, (int64_t)0, sp + g0, segK,
+                               segE, el, ev, sc, ring, out + g0 * TB);
+        KERNEL_CHECK();
+    }
+}
+
+}  // namespace
+
+void band_cov(System& S, const int32_t* h_perm, double* h_E, int64_t nops, const int64_t* h_rp, const int32_t* h_ci,
+              const double* h_v, double* h_oe, int64_t* info) {
+    hipStream_t st = S.stream;
+    refresh_scaling(S, S.cs_mode < 0 ? 0 : S.cs_mode);
+    const int64_t n = S.G.n;
+    if (n <= 0) throw std::invalid_argument("lsq_cov_band: empty system");
+    if (n >= INT_MAX) throw std::invalid_argument("lsq_cov_band: too many columns");
+    std::vector<int32_t> pinv(n, -1);
+    for (int64_t j = 0; j < n; ++j) {
+        const int32_t o = h_perm ? h_perm[j] : (int32_t)j;
+        if (o < 0 || o >= n || pinv[o] >= 0) throw std::invalid_argument("lsq_cov_band: perm is not a permutation of the columns");
+        pinv[o] = (int32_t)j;
+    }
+    for (int64_t i = 0; i < nops; ++i)
+        for (int64_t e = h_rp[i]; e < h_rp[i + 1]; ++e)
+            if (h_ci[e] < 0 || h_ci[e] >= n) throw std::invalid_argument("lsq_cov_band: op column out of range");
+    std::vector<int32_t> perm(n);
+    for (int64_t j = 0; j < n; ++j) perm[pinv[j]] = (int32_t)j;
+    const int64_t T = (n + TB - 1) / TB, npad = T * TB;
+    DBuf<int32_t> dperm(n), dpinv(n);
+    dperm.upload(perm.data(), n, st);
+    dpinv.upload(pinv.data(), n, st);
+    DBuf<int> wmax(1);
+    wmax.zero(st);
+    hipLaunchKernelGGL(k_band_width, dim3(grid_for(S.G.m)), dim3(BLOCK), 0, st, S.G.m, S.G.rp.p, S.G.ci.p, dpinv.p,
+                       S.rs.p, wmax.p);
+    KERNEL_CHECK();
+    int hw = 0;
+    HIP_CHECK(hipMemcpyAsync(&hw, wmax.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    const int w = (int)std::min<int64_t>(hw, T - 1);
+    const int64_t band_tiles = T * (int64_t)(w + 1);
+    const int64_t ring_wg = (int64_t)(w + 1) * TT * (int64_t)sizeof(double);
+    const int64_t bytes = (band_tiles + T) * TT * (int64_t)sizeof(double) + npad * 16;
+    size_t free_b = 0, total_b = 0;
+    HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+    const double avail = 0.9 * (double)free_b - (double)bytes;
+    if (avail < (double)ring_wg * 64)
+        throw std::invalid_argument("lsq_cov_band: band of " + std::to_string(w) + " tiles needs " +
+                                    std::to_string(bytes >> 20) + " MiB, more than the device has free");
+    // rings for up to `cap` concurrent workgroups (launches are batched beyond)
+    const int64_t nop_wg = (nops + TB - 1) / TB;
+    const int64_t cap = std::min<int64_t>({(int64_t)(0.5 * avail / ring_wg), std::max(T, nop_wg), 1 << 16});
+    DBuf<double> R(band_tiles * TT), D(T * TT), ring(cap * (w + 1) * TT);
+    R.zero(st);
+    BandDev b{T, w, R.p, D.p};
+    hipLaunchKernelGGL(k_band_normal, dim3(grid_for(npad)), dim3(BLOCK), 0, st, n, npad, b, dperm.p, dpinv.p,
+                       S.GT.rp.p, S.GT.ci.p, S.GT.val.p, S.G.rp.p, S.G.ci.p, S.G.val.p, S.rs.p);
+    KERNEL_CHECK();
+    DBuf<double> sc(npad);
+    hipLaunchKernelGGL(k_band_dscale, dim3(grid_for(npad)), dim3(BLOCK), 0, st, b, npad, sc.p);
+    hipLaunchKernelGGL(k_band_apply_scale, dim3(grid_for(band_tiles * TT)), dim3(BLOCK), 0, st, b, sc.p);
+    KERNEL_CHECK();
+    DBuf<int> err(1);
+    err.zero(st);
+    for (int64_t K = 0; K < T; ++K) {
+        hipLaunchKernelGGL(k_band_potrf, dim3(1), dim3(BLOCK), 0, st, b, K, err.p);
+        const int m = (int)std::min<int64_t>(w, T - 1 - K);
+        if (m > 0) {
+            hipLaunchKernelGGL(k_band_trsm, dim3(m), dim3(BLOCK), 0, st, b, K);
+            hipLaunchKernelGGL(k_band_syrk, dim3(m * m), dim3(BLOCK), 0, st, b, K, m);
+        }
+    }
+    KERNEL_CHECK();
+    int h_err = 0;
+    HIP_CHECK(hipMemcpyAsync(&h_err, err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (h_err) throw std::invalid_argument("lsq_cov_band: AᵀA is not positive definite (rank-deficient system)");
+    // the diagonal: identity right-hand sides, tile J from row J on
+    DBuf<double> ssq(npad), dE(n);
+    run_sweeps<true>(st, b, T, cap, nullptr, nullptr, nullptr, nullptr, nullptr, sc.p, ring.p, ssq.p);
+    hipLaunchKernelGGL(k_band_diag_sweep, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, dperm.p, ssq.p, sc.p, dE.p);
+    KERNEL_CHECK();
+    dE.download(h_E, n, st);
+    HIP_CHECK(hipStreamSynchronize(st));
+    int64_t products = 0;
+    for (int64_t J = 0; J < T; ++J) products += (T - J) * (int64_t)std::min<int64_t>(w + 1, T - J);
+    if (nops > 0) {
+        std::vector<int64_t> rows(nops);
+        for (int64_t i = 0; i < nops; ++i) rows[i] = i;
+        SweepOps so = sweep_ops(rows, h_rp, h_ci, h_v, pinv, T, w);
+        products += so.gemms;
+        const int64_t nwg = (int64_t)so.sp.size() - 1;
+        DBuf<int64_t> dsp(nwg + 1), dsegK((int64_t)so.segK.size()), dsegE((int64_t)so.segE.size());
+        DBuf<int32_t> del(std::max<int64_t>((int64_t)so.el.size(), 1));
+        DBuf<double> dev(std::max<int64_t>((int64_t)so.ev.size(), 1)), dout(nwg * TB);
+        dsp.upload(so.sp.data(), nwg + 1, st);
+        dsegK.upload(so.segK.data(), (int64_t)so.segK.size(), st);
+        dsegE.upload(so.segE.data(), (int64_t)so.segE.size(), st);
+        del.upload(so.el.data(), (int64_t)so.el.size(), st);
+        dev.upload(so.ev.data(), (int64_t)so.ev.size(), st);
+        run_sweeps<false>(st, b, nwg, cap, dsp.p, dsegK.p, dsegE.p, del.p, dev.p, sc.p, ring.p, dout.p);
+        std::vector<double> o(nwg * TB);
+        dout.download(o.data(), nwg * TB, st);
+        HIP_CHECK(hipStreamSynchronize(st));
+        for (int64_t i = 0; i < nops; ++i) h_oe[i] = std::sqrt(o[i]);
+    }
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (info) {
+        info[0] = w;
+        info[1] = T;
+        info[2] = bytes + ring.n * (int64_t)sizeof(double);
+        info[3] = products;
+    }
+}
+
+}  // namespace lsq

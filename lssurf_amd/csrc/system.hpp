@@ -347,7 +347,10 @@ void finish_formation(System& S);              // G set -> GT, SELL copies, defa
 void build_dmf(System& S, int32_t n_grids, const lsq_grid_desc* grids, int32_t n_interp, const int32_t* interp_grid,
                int64_t npts, const double* py, const double* px, const double* pt);   // S.dmf (CGNR data rows)
 void ensure_sell(System& S);                    // assembled A / AT (lazy when S.mf)
-void refresh_scaling(System& S, int precond);   // rs/cs -> SELL values (single GPU)
+void refresh_scaling(System& S, int precond);
+// band.hip: sqrt(diag((AᵀA)⁻¹)) and op-row variances from a banded Cholesky + Takahashi inverse
+void band_cov(System& S, const int32_t* perm, double* E, int64_t nops, const int64_t* rp, const int32_t* ci,
+              const double* v, double* op_err, int64_t* info);   // rs/cs -> SELL values (single GPU)
 void scaling_rows_colnorm(System& S, int precond, bool raw);
 void mf_column_scale(System& S, bool raw);       // lsqr.hip: column norms from the stencil structure
 void scaling_finish_cs(System& S);

@@ -8,6 +8,12 @@ E0 = sqrt(diag((AᵀA)⁻¹)) for any R with RᵀR = AᵀA, so lssurf_amd forms 
 factor R on the device (liblsqsurf dense path) and computes the row RSS of R⁻¹ there, without
 the 1e-5 drop tolerance (the reference's truncation changes E0 by ~sqrt(#dropped)·1e-5; see
 DESIGN.md §Parity).
+
+Default (`method='band'`): no dense factor — the columns are ordered by node position
+(`band_order`), AᵀA is factored inside its band and the rows of R⁻¹ are formed by banded forward
+sweeps without being stored (liblsqsurf `lsq_cov_band`, csrc/band.hip); the averaging operators'
+errors sqrt(diag(op (AᵀA)⁻¹ opᵀ)) come from sweeps with the op rows as right-hand sides.
+`method='dense'` keeps the n × n factor and R⁻¹ (n ≲ 3·10⁴).
 """
 from time import time
 
@@ -18,19 +24,71 @@ from . import containers as pc
 from .smooth_fit import FitSystem
 
 
-def calc_and_parse_errors(E, G_data, Gc, Ed, Ec, data, in_TSE, keep_cols, grids, avg_ops, device=0, timing=None):
+def band_order(grids, keep_cols):
+    """New position -> compact column: columns ordered by node position (y, then x), then grid,
+    then epoch, so that AᵀA of a smooth_fit system is banded (z0 and dz of a node adjacent, a band
+    of ~2 node rows).  Columns outside every grid go last."""
+    gl = [g for g in grids.values() if getattr(g, 'N_dims', 0) >= 2]
+    n_full = max(int(g.col_N) for g in gl)
+    key = np.full((4, n_full), np.inf)
+    for gi, g in enumerate(gl):
+        sub = np.unravel_index(np.arange(int(g.N_nodes)), tuple(g.shape))
+        idx = np.arange(g.col_0, g.col_0 + int(g.N_nodes))
+        key[0, idx] = g.ctrs[0][sub[0]]
+        key[1, idx] = g.ctrs[1][sub[1]]
+        key[2, idx] = gi
+        key[3, idx] = sub[2] if g.N_dims > 2 else -1
+    k = key[:, keep_cols]
+    return np.lexsort((k[3], k[2], k[1], k[0])).astype(np.int32)
+
+
+def _compact_rows(op, keep_cols, n_full):
+    """The op's CSR (rows = its output equations) over the compact columns: entries in removed
+    columns dropped (Ip_c·Rinv has zero rows there, smooth_fit.py:266)."""
+    rows = op.ind0 if op.dst_ind0 is None else op.dst_ind0
+    A = op.toCSR(row_N=rows.size, col_N=n_full).tocsc()
+    return A[:, keep_cols].tocsr()
+
+
+def _grid_values(op, vals):
+    """Place per-row values on the op's output grid (the layout of lin_op.grid_error)."""
+    grid, rows = op._out_grid_and_rows(None)
+    E = np.zeros(op.col_N) + np.nan
+    E[rows] = vals
+    return E[grid.col_0:grid.col_N].reshape(grid.shape)
+
+
+def calc_and_parse_errors(E, G_data, Gc, Ed, Ec, data, in_TSE, keep_cols, grids, avg_ops, device=0, timing=None,
+                          method='band'):
     timing = {} if timing is None else timing
     tic = time()
     sigma_data = np.sqrt(Ed ** 2 + data.sigma_extra ** 2)
     E_all = np.concatenate((sigma_data, Ec))
     w = 1. / E_all                                   # TCinv, smooth_fit.py:697
     fs = FitSystem(G_data, Gc, keep_cols, Gc.col_N, device=device)
+    op_err = {}
     try:
         fs.solver.set_row_weight(w)
         fs.solver.set_row_mask(np.concatenate([np.asarray(in_TSE, bool), np.ones(Gc.N_eq, bool)]))
-        E0c = fs.solver.sigma_x()
-        timing['decompose_qz'] = time() - tic
-        Rinv = fs.solver.rinv() if avg_ops else None
+        if method == 'band':
+            keys = list(avg_ops)
+            mats = [_compact_rows(avg_ops[k], keep_cols, Gc.col_N) for k in keys]
+            op = sp.vstack(mats).tocsr() if mats else None
+            E0c, errs, info = fs.solver.cov_band(band_order(grids, keep_cols), op)
+            timing['decompose_qz'] = time() - tic
+            timing['E_band'] = {'tiles': int(info[0]), 'tile_rows': int(info[1]), 'bytes': int(info[2]),
+                                'tile_products': int(info[3])}
+            off = 0
+            for k, m in zip(keys, mats):
+                op_err[k] = errs[off:off + m.shape[0]]
+                off += m.shape[0]
+            Rinv = None
+        elif method == 'dense':
+            E0c = fs.solver.sigma_x()
+            timing['decompose_qz'] = time() - tic
+            Rinv = fs.solver.rinv() if avg_ops else None
+        else:
+            raise ValueError(f'calc_and_parse_errors: unknown method {method!r}')
     finally:
         fs.close()
     timing['propagate_errors'] = time() - tic
@@ -42,10 +100,12 @@ def calc_and_parse_errors(E, G_data, Gc, Ed, Ec, data, in_TSE, keep_cols, grids,
     E['sigma_dz'] = pc.grid.data().from_dict({'x': dzg.ctrs[1], 'y': dzg.ctrs[0], 'time': dzg.ctrs[2],
                                               'sigma_dz': np.reshape(E0[Gc.TOC['cols']['dz']], dzg.shape)})
     if avg_ops:
-        full = np.zeros((Gc.col_N, Rinv.shape[1]))
-        full[keep_cols] = Rinv                       # Ip_c · Rinv
+        if Rinv is not None:
+            full = np.zeros((Gc.col_N, Rinv.shape[1]))
+            full[keep_cols] = Rinv                   # Ip_c · Rinv
+            Rs = sp.csr_matrix(full)
         for key, op in avg_ops.items():
             fields = {coord: ctr for coord, ctr in zip(op.dst_grid.coords, op.dst_grid.ctrs)}
-            fields['sigma_' + key] = op.grid_error(sp.csr_matrix(full))
+            fields['sigma_' + key] = op.grid_error(Rs) if Rinv is not None else _grid_values(op, op_err[key])
             E['sigma_' + key] = pc.grid.data().from_dict(fields)
     return E

@@ -47,7 +47,8 @@ DEFAULTS = {'reference_epoch': 0, 'W_ctr': 1e4, 'return_fit_objects': False, 'ma
             # lssurf_amd solver options (new keys; defaults reproduce the exact LS solution to
             # the tolerance documented in DESIGN.md §Parity)
             'device': 0, 'lsq_atol': 1e-12, 'lsq_btol': 1e-12, 'lsq_conlim': 1e12, 'lsq_maxit': 0,
-            'lsq_precond': 'auto', 'lsq_dense_max': 16384, 'lsq_warm_start': True, 'lsq_method': 'auto'}
+            'lsq_precond': 'auto', 'lsq_dense_max': 16384, 'lsq_warm_start': True, 'lsq_method': 'auto',
+            'lsq_E_method': 'band'}
 
 OUT_OF_SCOPE = ('bias_params', 'sensor_grid_bias_params', 'prior_args', 'prior_edge_args', 'lagrangian_coords',
                 'constraint_scaling_maps', 'mask_file', 'bias_edit_vals')
@@ -460,7 +461,7 @@ def smooth_fit(**kwargs):
                 print('Starting uncertainty calculation', flush=True)
                 tic_error = time()
             calc_and_parse_errors(E, G_data, Gc, Ed, Ec, data, in_TSE, keep_cols, grids, averaging_ops,
-                                  device=args['device'], timing=timing)
+                                  device=args['device'], timing=timing, method=args['lsq_E_method'])
             if args['VERBOSE']:
                 print('\tUncertainty propagation took %3.2f seconds' % (time() - tic_error), flush=True)
     finally:

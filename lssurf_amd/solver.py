@@ -225,6 +225,28 @@ class LSQSolver:
         self._check(self._L.lsq_get_rinv(self._h, ptr(Ri)), 'lsq_get_rinv')
         return Ri
 
+    def cov_band(self, perm=None, op=None):
+        """(E, op_err, info) of the current weighted, masked system without a dense factor:
+        E = sqrt(diag((AᵀA)⁻¹)) per compact column and, for the rows of `op` (scipy sparse over
+        the compact columns), sqrt(diag(op (AᵀA)⁻¹ opᵀ)).  `perm` (new position -> compact column)
+        should make AᵀA banded (lsq_cov_band)."""
+        E = np.zeros(self.n)
+        info = np.zeros(4, np.int64)
+        pp = None if perm is None else as_c(perm, np.int32)
+        if pp is not None and pp.size != self.n:
+            raise ValueError('cov_band: perm must have one entry per column')
+        if op is None:
+            self._check(self._L.lsq_cov_band(self._h, ptr(pp) if pp is not None else None, ptr(E), 0, None, None,
+                                             None, None, ptr(info)), 'lsq_cov_band')
+            return E, None, info
+        op = sp.csr_matrix(op)
+        op.sort_indices()
+        rp, ci, v = as_c(op.indptr, np.int64), as_c(op.indices, np.int32), as_c(op.data, np.float64)
+        out = np.zeros(op.shape[0])
+        self._check(self._L.lsq_cov_band(self._h, ptr(pp) if pp is not None else None, ptr(E), op.shape[0],
+                                         ptr(rp), ptr(ci), ptr(v), ptr(out), ptr(info)), 'lsq_cov_band')
+        return E, out, info
+
     def spmv(self, x, trans=False):
         """G x (trans False) or Gᵀ x on the UNWEIGHTED formed operator, all rows."""
         x = as_c(x, np.float64)
