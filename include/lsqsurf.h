@@ -53,7 +53,8 @@ typedef struct lsq_opts {
                            /*     SURVEY.md §8 a7.4 — no reference counterpart), 4 = geometric  */
                            /*     multigrid V-cycle over the (y, x) node lattice (method 1,     */
                            /*     single-GPU smooth_fit systems with per-node column blocks;    */
-                           /*     DESIGN.md §Multigrid)                                         */
+                           /*     DESIGN.md §Multigrid), 5 = banded Cholesky R̃⁻¹ in the order of */
+                           /*     lsq_set_band_order (LSQR, single GPU; band.hip)               */
     double  atol, btol, conlim;
     int64_t maxit;
     int32_t use_x0;        /* 1: x_inout holds a warm start (outer-iteration "resume")          */
@@ -180,6 +181,15 @@ int lsq_iterate(lsq_handle* h, const double* b, int64_t iters, const lsq_opts* o
  * lsq_get_rinv: R^-1 as a dense n x n row-major upper-triangular matrix. */
 int lsq_sigma_x(lsq_handle* h, double* E);
 int lsq_get_rinv(lsq_handle* h, double* Rinv);
+/* Column order for precond 5 (band factor): perm[j] = the compact column at position j, chosen so
+ * that AᵀA is banded (a grid system: its natural row-major order; others: e.g. reverse
+ * Cuthill-McKee).  nullptr = natural order.  Precond 5 (LSQR on the assembled operator,
+ * single GPU): M = P·S·R̃⁻¹ with R̃ the banded Cholesky factor of the equilibrated S·PᵀAᵀAP·S
+ * (band.hip), applied by one band back / forward substitution per product — the large-n
+ * counterpart of precond 2, for systems column scaling cannot precondition (the anisotropic
+ * notebook: > 5·10⁴ column-scaled iterations).  Refused when the band is wider than 300 tiles. */
+int lsq_set_band_order(lsq_handle* h, int64_t n, const int32_t* perm);
+
 /* Error propagation without a dense factor (replaces sparseqr.rz + inv_tr_upper +
  * propagate_qz_errors at smooth_fit.py:218-253 and op.grid_error(Ip_c·Rinv) at :266-270).
  * perm (length n, nullable = identity): new position j -> compact column perm[j]; an order in

@@ -255,7 +255,8 @@ int lsq_solve(lsq_handle* h, const double* b, double* x_inout, const lsq_opts* o
         lsq_default_opts(&d);
         if (!o) o = &d;
         if (o->method != 0 && o->method != 1) return fail(S, "lsq_solve: method must be 0 (LSQR) or 1 (CGNR)");
-        if (o->precond < 0 || o->precond > 4) return fail(S, "lsq_solve: precond must be 0, 1, 2, 3 or 4");
+        if (o->precond < 0 || o->precond > 5) return fail(S, "lsq_solve: precond must be 0 .. 5");
+        if (o->precond == 5 && S.dist) return fail(S, "lsq_solve: precond 5 (band factor) is single-GPU");
         if (o->precond == 4 && (o->method != 1 || S.dist || !lsq::cg_available(S, 4)))
             return fail(S, "lsq_solve: precond 4 (multigrid) runs CGNR (method 1) on single-GPU structured systems: " +
                                (S.dist ? std::string("distributed rank") : o->method != 1 ? std::string("method is not 1") : S.cg_ok ? S.mg_why : S.cg_why));
@@ -528,6 +529,22 @@ int lsq_sigma_x(lsq_handle* h, double* E) {
         if (!S.G.rp.p) return fail(S, "lsq_sigma_x: no matrix");
         if (!E) return fail(S, "lsq_sigma_x: null output");
         lsq::lsqr_sigma_x(S, E);
+        return 0;
+    });
+}
+
+int lsq_set_band_order(lsq_handle* h, int64_t n, const int32_t* perm) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_set_band_order: no matrix");
+        if (perm && n != S.G.n) return fail(S, "lsq_set_band_order: the order needs one entry per column");
+        std::vector<char> seen(perm ? n : 0, 0);
+        for (int64_t j = 0; perm && j < n; ++j) {
+            if (perm[j] < 0 || perm[j] >= n || seen[perm[j]]) return fail(S, "lsq_set_band_order: not a permutation");
+            seen[perm[j]] = 1;
+        }
+        S.band_order.assign(perm ? perm : nullptr, perm ? perm + n : nullptr);
+        S.band.valid = false;
+        S.iter_ready = false;
         return 0;
     });
 }

@@ -198,76 +198,77 @@ __global__ __launch_bounds__(BLOCK) void k_band_apply_scale(BandDev b, const dou
     }
 }
 
-// POTRF of tile (K, K) in LDS (as dense.hip's k_potrf_diag), then D_K = R_KK⁻¹ (column-parallel
-// back substitution); the lower triangle of R_KK is zeroed
-__global__ __launch_bounds__(BLOCK) void k_band_potrf(BandDev b, int64_t K, int* err) {
-    __shared__ double A[TB * LDP];
-    __shared__ double X[TB * LDP];
+// broadcast lane l's double (two readlanes into scalar registers)
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)u, l), hi = __builtin_amdgcn_readlane((int)(u >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// POTRF of tile (K, K) and D_K = R_KK⁻¹ by ONE wave, lane k holding column k of the tile in
+// registers: no barriers, row j of R broadcast lane by lane with readlane.  Measured per tile:
+// 77 µs (the 256-thread LDS version with 192 barriers: 128 µs; LDS broadcasts within one wave:
+// 140 µs).  The lower triangle is zeroed.
+__global__ __launch_bounds__(TB) void k_band_potrf(BandDev b, int64_t K, int* err) {
+    const int k = threadIdx.x;
     double* Rt = btile(b.R, b.w, K, K);
-    for (int idx = threadIdx.x; idx < TT; idx += BLOCK) {
-        const int r = idx >> 6, c = idx & 63;
-        A[r * LDP + c] = c >= r ? Rt[idx] : 0.0;
-        X[r * LDP + c] = 0.0;
-    }
-    __syncthreads();
+    double a[TB];
+#pragma unroll
+    for (int i = 0; i < TB; ++i) a[i] = i <= k ? Rt[i * TB + k] : 0.0;
+    bool bad = false;
+#pragma unroll
     for (int j = 0; j < TB; ++j) {
-        if (threadIdx.x == 0) {
-            const double d = A[j * LDP + j];
-            if (!(d > 0.0)) {
-                atomicExch(err, 1);
-                A[j * LDP + j] = 1.0;
-            } else {
-                A[j * LDP + j] = sqrt(d);
-            }
-        }
-        __syncthreads();
-        const double piv = A[j * LDP + j];
-        for (int k = j + 1 + threadIdx.x; k < TB; k += BLOCK) A[j * LDP + k] /= piv;
-        __syncthreads();
-        for (int idx = threadIdx.x; idx < TT; idx += BLOCK) {
-            const int i = idx >> 6, k = idx & 63;
-            if (i > j && k >= i) A[i * LDP + k] -= A[j * LDP + i] * A[j * LDP + k];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x < TB) {
-        const int c = threadIdx.x;
-        for (int i = c; i >= 0; --i) {
-            double x = (i == c) ? 1.0 : 0.0;
-            for (int j = i + 1; j <= c; ++j) x -= A[i * LDP + j] * X[j * LDP + c];
-            X[i * LDP + c] = x / A[i * LDP + i];
+        const double d = readlane_d(a[j], j);
+        double r = 1.0;
+        if (d > 0.0) r = sqrt(d);
+        else bad = true;
+        a[j] = k == j ? r : (k > j ? a[j] / r : 0.0);   // row j of R (column k's entry)
+#pragma unroll
+        for (int i = j + 1; i < TB; ++i) {
+            const double rji = readlane_d(a[j], i);
+            if (k >= i) a[i] -= rji * a[j];
         }
     }
-    __syncthreads();
+    if (bad && k == 0) atomicExch(err, 1);
+    double x[TB];   // column k of D = R⁻¹: R x = e_k by back substitution
+#pragma unroll
+    for (int i = TB - 1; i >= 0; --i) {
+        double s = i == k ? 1.0 : 0.0;
+#pragma unroll
+        for (int j = i + 1; j < TB; ++j) s -= readlane_d(a[i], j) * x[j];
+        x[i] = s / readlane_d(a[i], i);
+    }
     double* Dk = b.D + K * TT;
-    for (int idx = threadIdx.x; idx < TT; idx += BLOCK) {
-        const int r = idx >> 6, c = idx & 63;
-        Rt[idx] = A[r * LDP + c];
-        Dk[idx] = X[r * LDP + c];
+#pragma unroll
+    for (int i = 0; i < TB; ++i) {
+        Rt[i * TB + k] = a[i];
+        Dk[i * TB + k] = x[i];
     }
 }
 
-// R_KJ = R_KK⁻ᵀ N_KJ for J = K+1..K+m (one workgroup per tile), by forward substitution as
-// dense.hip's k_trsm_panel: multiplying by the explicit D_Kᵀ instead loses ~cond(R_KK)·ε per tile
-// row and compounds over the factor (measured 1e-6 on E at 48²×12 against 3e-13 here)
-__global__ __launch_bounds__(BLOCK) void k_band_trsm(BandDev b, int64_t K) {
-    __shared__ double R[TB * LDP];
-    __shared__ double X[TB * LDP];
+// R_KJ = R_KK⁻ᵀ N_KJ for J = K+1..K+m (one wave per tile, lane c holding column c of the tile
+// in registers) by forward substitution with R_KK broadcast from LDS.  Multiplying by the
+// explicit D_Kᵀ instead would lose ~cond(R_KK)·ε per tile row.
+__global__ __launch_bounds__(TB) void k_band_trsm(BandDev b, int64_t K) {
+    __shared__ double R[TT];
+    __shared__ double rdiag[TB];
+    const int c = threadIdx.x;
+    const double* Rkk = btile(b.R, b.w, K, K);
+    for (int idx = c; idx < TT; idx += TB) R[idx] = Rkk[idx];
+    rdiag[c] = b.D[K * TT + c * TB + c];   // 1/R_cc (D_K's diagonal, one correctly rounded division)
     double* Nt = btile(b.R, b.w, K, K + 1 + blockIdx.x);
-    lds_tile<false>(R, btile(b.R, b.w, K, K));
-    lds_tile<false>(X, Nt);
+    double x[TB];
+#pragma unroll
+    for (int i = 0; i < TB; ++i) x[i] = Nt[i * TB + c];
     __syncthreads();
+#pragma unroll
     for (int i = 0; i < TB; ++i) {
-        const double piv = R[i * LDP + i];
-        if (threadIdx.x < TB) X[i * LDP + threadIdx.x] /= piv;
-        __syncthreads();
-        for (int idx = threadIdx.x; idx < TT; idx += BLOCK) {
-            const int p = idx >> 6, c = idx & 63;
-            if (p > i) X[p * LDP + c] -= R[i * LDP + p] * X[i * LDP + c];
-        }
-        __syncthreads();
+        x[i] *= rdiag[i];
+#pragma unroll
+        for (int p = i + 1; p < TB; ++p) x[p] -= R[i * TB + p] * x[i];
     }
-    for (int idx = threadIdx.x; idx < TT; idx += BLOCK) Nt[idx] = X[(idx >> 6) * LDP + (idx & 63)];
+#pragma unroll
+    for (int i = 0; i < TB; ++i) Nt[i * TB + c] = x[i];
 }
 
 // N_{K+a, K+c} −= R_{K,K+a}ᵀ R_{K,K+c}, 1 ≤ a ≤ c ≤ m (grid m·m, lower pairs idle)
@@ -376,6 +377,122 @@ __global__ __launch_bounds__(BLOCK) void k_band_diag_sweep(int64_t n, const int3
         E[perm[j]] = sqrt(ssq[j]) * sc[j];
 }
 
+// ---- precond 5: LSQR on A·M, M = P·S·R̃⁻¹ (lsqr.hip) ------------------------------------------
+// One workgroup walks the band tile row by tile row (a triangular solve is a chain of T dependent
+// steps); the last w+1 solved tiles stay in an LDS ring, the band tiles stream from HBM with each
+// thread owning a 16-wide segment of one row (bsub) or column (fsub) of every tile.
+
+// out = M·v·scale: x̃ = R̃⁻¹ v by back substitution, x̃_K = D_K (v_K − Σ_{J=K+1}^{K+w} R̃_KJ x̃_J),
+// out[perm[j]] = sc_j x̃_j.  scale_mode 1: v / α (and nothing once the solve stopped), 2: v.
+__global__ __launch_bounds__(BLOCK) void k_band_bsub(const double* __restrict__ R, const double* __restrict__ D,
+                                                     int64_t T, int w, int64_t n, const double* __restrict__ v,
+                                                     const LsqState* __restrict__ st, int scale_mode,
+                                                     const double* __restrict__ sc, const int32_t* __restrict__ perm,
+                                                     double* __restrict__ out) {
+    if (st && st->stop && scale_mode != 2) return;
+    extern __shared__ double ring[];   // (w+1) × 64
+    __shared__ double Y[TB];
+    const double scale = scale_mode == 1 ? st->inv_alpha : 1.0;
+    const int t = threadIdx.x, r = t >> 2, q = t & 3;
+    for (int64_t K = T - 1; K >= 0; --K) {
+        double acc = 0.0;
+        const int64_t J1 = min<int64_t>(K + w, T - 1);
+        for (int64_t J = K + 1; J <= J1; ++J) {
+            const double2* Rt = reinterpret_cast<const double2*>(R + ((K * (w + 1)) + (J - K)) * TT + r * TB + q * 16);
+            const double* xs = ring + (J % (w + 1)) * TB + q * 16;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const double2 a = Rt[c];
+                acc += a.x * xs[2 * c] + a.y * xs[2 * c + 1];
+            }
+        }
+        acc += __shfl_xor(acc, 1);
+        acc += __shfl_xor(acc, 2);
+        const int64_t j = K * TB + r;
+        if (q == 0) Y[r] = (j < n ? v[j] * scale : 0.0) - acc;
+        __syncthreads();
+        const double* Dr = D + K * TT + r * TB + q * 16;   // x̃_K = D_K Y (D upper)
+        double x = 0.0;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) x += Dr[c] * Y[q * 16 + c];
+        x += __shfl_xor(x, 1);
+        x += __shfl_xor(x, 2);
+        if (q == 0) {
+            ring[(K % (w + 1)) * TB + r] = x;
+            if (j < n) out[perm[j]] = sc[j] * x;
+        }
+        __syncthreads();
+    }
+}
+
+// vout = R̃⁻ᵀ (S Pᵀ t) with LSQR's epilogue (as dense.hip's k_gemvT_upper mode 1):
+// ỹ_K = D_Kᵀ (t̃_K − Σ_{I=K−w}^{K−1} R̃_IKᵀ ỹ_I), vout_j = ỹ_j/β − β vin_j/α (vin_j when β = 0),
+// part[0] = Σ vout².
+__global__ __launch_bounds__(BLOCK) void k_band_fsub(const double* __restrict__ R, const double* __restrict__ D,
+                                                     int64_t T, int w, int64_t n, const double* __restrict__ tin,
+                                                     const LsqState* __restrict__ st, const double* __restrict__ vin,
+                                                     double* __restrict__ vout, const double* __restrict__ sc,
+                                                     const int32_t* __restrict__ perm, double* __restrict__ part) {
+    if (st && st->stop) return;
+    extern __shared__ double ring[];   // (w+1) × 64
+    __shared__ double Z[TB];
+    __shared__ double P4[4][TB];
+    __shared__ double red[4];
+    const int t = threadIdx.x, c = t & 63, q = t >> 6;   // column c, rows q*16 .. q*16+15
+    double sv = 0.0;
+    for (int64_t K = 0; K < T; ++K) {
+        double acc = 0.0;
+        for (int64_t I = max<int64_t>(0, K - w); I < K; ++I) {
+            const double* Rt = R + ((I * (w + 1)) + (K - I)) * TT + (q * 16) * TB + c;
+            const double* ys = ring + (I % (w + 1)) * TB + q * 16;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc += Rt[r * TB] * ys[r];
+        }
+        P4[q][c] = acc;
+        __syncthreads();
+        const int64_t j = K * TB + c;
+        if (q == 0) Z[c] = (j < n ? tin[perm[j]] * sc[j] : 0.0) - ((P4[0][c] + P4[1][c]) + (P4[2][c] + P4[3][c]));
+        __syncthreads();
+        const double* Dc = D + K * TT + (q * 16) * TB + c;   // (D_Kᵀ Z)_c = Σ_r D[r][c] Z[r]
+        double y = 0.0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) y += Dc[r * TB] * Z[q * 16 + r];
+        P4[q][c] = y;
+        __syncthreads();
+        if (q == 0) {
+            const double yc = (P4[0][c] + P4[1][c]) + (P4[2][c] + P4[3][c]);
+            ring[(K % (w + 1)) * TB + c] = yc;
+            if (j < n) {
+                const double o = st->skip_v ? vin[j] : yc * st->inv_beta - st->beta * (vin[j] * st->inv_alpha);
+                vout[j] = o;
+                sv += o * o;
+            }
+        }
+        __syncthreads();
+    }
+    const double s = block_sum(sv, red);
+    if (threadIdx.x == 0) part[0] = s;
+}
+
+// warm start y0 = M⁻¹ x0 = R̃ S⁻¹ Pᵀ x0 (one thread per row of R̃)
+__global__ __launch_bounds__(BLOCK) void k_band_warm(const double* __restrict__ R, int64_t T, int w, int64_t n,
+                                                     const double* __restrict__ x0, const double* __restrict__ sc,
+                                                     const int32_t* __restrict__ perm, double* __restrict__ y0) {
+    for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLOCK) {
+        const int64_t I = j >> 6;
+        const int rj = (int)(j & 63);
+        double s = 0.0;
+        for (int64_t J = I; J <= min<int64_t>(I + w, T - 1); ++J) {
+            const double* row = R + ((I * (w + 1)) + (J - I)) * TT + rj * TB;
+            for (int c = (J == I ? rj : 0); c < TB; ++c) {
+                const int64_t k = J * TB + c;
+                if (k < n) s += row[c] * (x0[perm[k]] / sc[k]);
+            }
+        }
+        y0[j] = s;
+    }
+}
+
 }  // namespace
 
 namespace {
@@ -435,27 +552,24 @@ void run_sweeps(hipStream_t st, const BandDev& b, int64_t nwg, int64_t cap, cons
 
 }  // namespace
 
-void band_cov(System& S, const int32_t* h_perm, double* h_E, int64_t nops, const int64_t* h_rp, const int32_t* h_ci,
-              const double* h_v, double* h_oe, int64_t* info) {
+// AᵀA of the current weighted, masked system in the order h_perm (nullable: natural), equilibrated
+// and factored inside its band into F
+void band_factor(System& S, const int32_t* h_perm, BandFactor& F) {
     hipStream_t st = S.stream;
-    refresh_scaling(S, S.cs_mode < 0 ? 0 : S.cs_mode);
     const int64_t n = S.G.n;
-    if (n <= 0) throw std::invalid_argument("lsq_cov_band: empty system");
-    if (n >= INT_MAX) throw std::invalid_argument("lsq_cov_band: too many columns");
-    std::vector<int32_t> pinv(n, -1);
+    if (n <= 0) throw std::invalid_argument("band factor: empty system");
+    if (n >= INT_MAX) throw std::invalid_argument("band factor: too many columns");
+    std::vector<int32_t> pinv(n, -1), perm(n);
     for (int64_t j = 0; j < n; ++j) {
         const int32_t o = h_perm ? h_perm[j] : (int32_t)j;
-        if (o < 0 || o >= n || pinv[o] >= 0) throw std::invalid_argument("lsq_cov_band: perm is not a permutation of the columns");
+        if (o < 0 || o >= n || pinv[o] >= 0) throw std::invalid_argument("band factor: the order is not a permutation of the columns");
         pinv[o] = (int32_t)j;
+        perm[j] = o;
     }
-    for (int64_t i = 0; i < nops; ++i)
-        for (int64_t e = h_rp[i]; e < h_rp[i + 1]; ++e)
-            if (h_ci[e] < 0 || h_ci[e] >= n) throw std::invalid_argument("lsq_cov_band: op column out of range");
-    std::vector<int32_t> perm(n);
-    for (int64_t j = 0; j < n; ++j) perm[pinv[j]] = (int32_t)j;
     const int64_t T = (n + TB - 1) / TB, npad = T * TB;
-    DBuf<int32_t> dperm(n), dpinv(n);
-    dperm.upload(perm.data(), n, st);
+    DBuf<int32_t> dpinv(n);
+    F.perm.alloc(n);
+    F.perm.upload(perm.data(), n, st);
     dpinv.upload(pinv.data(), n, st);
     DBuf<int> wmax(1);
     wmax.zero(st);
@@ -467,34 +581,34 @@ void band_cov(System& S, const int32_t* h_perm, double* h_E, int64_t nops, const
     HIP_CHECK(hipStreamSynchronize(st));
     const int w = (int)std::min<int64_t>(hw, T - 1);
     const int64_t band_tiles = T * (int64_t)(w + 1);
-    const int64_t ring_wg = (int64_t)(w + 1) * TT * (int64_t)sizeof(double);
-    const int64_t bytes = (band_tiles + T) * TT * (int64_t)sizeof(double) + npad * 16;
+    const int64_t bytes = (band_tiles + T) * TT * (int64_t)sizeof(double);
     size_t free_b = 0, total_b = 0;
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-    const double avail = 0.9 * (double)free_b - (double)bytes;
-    if (avail < (double)ring_wg * 64)
-        throw std::invalid_argument("lsq_cov_band: band of " + std::to_string(w) + " tiles needs " +
+    if ((double)bytes > 0.85 * (double)free_b)
+        throw std::invalid_argument("band factor: a band of " + std::to_string(w) + " tiles needs " +
                                     std::to_string(bytes >> 20) + " MiB, more than the device has free");
-    // rings for up to `cap` concurrent workgroups (launches are batched beyond)
-    const int64_t nop_wg = (nops + TB - 1) / TB;
-    const int64_t cap = std::min<int64_t>({(int64_t)(0.5 * avail / ring_wg), std::max(T, nop_wg), 1 << 16});
-    DBuf<double> R(band_tiles * TT), D(T * TT), ring(cap * (w + 1) * TT);
-    R.zero(st);
-    BandDev b{T, w, R.p, D.p};
-    hipLaunchKernelGGL(k_band_normal, dim3(grid_for(npad)), dim3(BLOCK), 0, st, n, npad, b, dperm.p, dpinv.p,
+    F.valid = false;
+    F.n = n;
+    F.T = T;
+    F.w = w;
+    F.R.alloc(band_tiles * TT);
+    F.D.alloc(T * TT);
+    F.sc.alloc(npad);
+    F.R.zero(st);
+    BandDev b{T, w, F.R.p, F.D.p};
+    hipLaunchKernelGGL(k_band_normal, dim3(grid_for(npad)), dim3(BLOCK), 0, st, n, npad, b, F.perm.p, dpinv.p,
                        S.GT.rp.p, S.GT.ci.p, S.GT.val.p, S.G.rp.p, S.G.ci.p, S.G.val.p, S.rs.p);
     KERNEL_CHECK();
-    DBuf<double> sc(npad);
-    hipLaunchKernelGGL(k_band_dscale, dim3(grid_for(npad)), dim3(BLOCK), 0, st, b, npad, sc.p);
-    hipLaunchKernelGGL(k_band_apply_scale, dim3(grid_for(band_tiles * TT)), dim3(BLOCK), 0, st, b, sc.p);
+    hipLaunchKernelGGL(k_band_dscale, dim3(grid_for(npad)), dim3(BLOCK), 0, st, b, npad, F.sc.p);
+    hipLaunchKernelGGL(k_band_apply_scale, dim3(grid_for(band_tiles * TT)), dim3(BLOCK), 0, st, b, F.sc.p);
     KERNEL_CHECK();
     DBuf<int> err(1);
     err.zero(st);
     for (int64_t K = 0; K < T; ++K) {
-        hipLaunchKernelGGL(k_band_potrf, dim3(1), dim3(BLOCK), 0, st, b, K, err.p);
+        hipLaunchKernelGGL(k_band_potrf, dim3(1), dim3(TB), 0, st, b, K, err.p);
         const int m = (int)std::min<int64_t>(w, T - 1 - K);
         if (m > 0) {
-            hipLaunchKernelGGL(k_band_trsm, dim3(m), dim3(BLOCK), 0, st, b, K);
+            hipLaunchKernelGGL(k_band_trsm, dim3(m), dim3(TB), 0, st, b, K);
             hipLaunchKernelGGL(k_band_syrk, dim3(m * m), dim3(BLOCK), 0, st, b, K, m);
         }
     }
@@ -502,11 +616,77 @@ void band_cov(System& S, const int32_t* h_perm, double* h_E, int64_t nops, const
     int h_err = 0;
     HIP_CHECK(hipMemcpyAsync(&h_err, err.p, sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
-    if (h_err) throw std::invalid_argument("lsq_cov_band: AᵀA is not positive definite (rank-deficient system)");
+    if (h_err) throw std::invalid_argument("band factor: AᵀA is not positive definite (rank-deficient system)");
+    F.valid = true;
+}
+
+// precond 5 needs the ring of w+1 tile vectors in LDS
+constexpr int BAND_PRECOND_WMAX = 300;
+
+void band_precond(System& S) {
+    band_factor(S, S.band_order.empty() ? nullptr : S.band_order.data(), S.band);
+    if (S.band.w > BAND_PRECOND_WMAX) {
+        S.band.valid = false;
+        throw std::invalid_argument("precond 5: the band of AᵀA is " + std::to_string(S.band.w) +
+                                    " tiles wide (at most " + std::to_string(BAND_PRECOND_WMAX) +
+                                    "); set a bandwidth-reducing order (lsq_set_band_order)");
+    }
+}
+
+void band_launch_bsub(System& S, const double* v, int scale_mode, double* out) {
+    const BandFactor& F = S.band;
+    hipLaunchKernelGGL(k_band_bsub, dim3(1), dim3(BLOCK), sizeof(double) * TB * (F.w + 1), S.stream, F.R.p, F.D.p, F.T,
+                       F.w, F.n, v, S.st.p, scale_mode, F.sc.p, F.perm.p, out);
+}
+
+void band_launch_fsub(System& S, const double* t, const double* vin, double* vout, double* part) {
+    const BandFactor& F = S.band;
+    hipLaunchKernelGGL(k_band_fsub, dim3(1), dim3(BLOCK), sizeof(double) * TB * (F.w + 1), S.stream, F.R.p, F.D.p, F.T,
+                       F.w, F.n, t, S.st.p, vin, vout, F.sc.p, F.perm.p, part);
+}
+
+void band_launch_warm(System& S, const double* x0, double* y0) {
+    const BandFactor& F = S.band;
+    hipLaunchKernelGGL(k_band_warm, dim3(grid_for(F.n)), dim3(BLOCK), 0, S.stream, F.R.p, F.T, F.w, F.n, x0, F.sc.p,
+                       F.perm.p, y0);
+}
+
+void band_cov(System& S, const int32_t* h_perm, double* h_E, int64_t nops, const int64_t* h_rp, const int32_t* h_ci,
+              const double* h_v, double* h_oe, int64_t* info) {
+    hipStream_t st = S.stream;
+    refresh_scaling(S, S.cs_mode < 0 ? 0 : S.cs_mode);
+    const int64_t n = S.G.n;
+    for (int64_t i = 0; i < nops; ++i)
+        for (int64_t e = h_rp[i]; e < h_rp[i + 1]; ++e)
+            if (h_ci[e] < 0 || h_ci[e] >= n) throw std::invalid_argument("lsq_cov_band: op column out of range");
+    BandFactor F;
+    band_factor(S, h_perm, F);
+    const int64_t T = F.T, npad = T * TB;
+    const int w = F.w;
+    std::vector<int32_t> pinv(n);
+    {
+        std::vector<int32_t> perm(n);
+        F.perm.download(perm.data(), n, st);
+        HIP_CHECK(hipStreamSynchronize(st));
+        for (int64_t j = 0; j < n; ++j) pinv[perm[j]] = (int32_t)j;
+    }
+    BandDev b{T, w, F.R.p, F.D.p};
+    const int64_t ring_wg = (int64_t)(w + 1) * TT * (int64_t)sizeof(double);
+    const int64_t bytes = (T * (int64_t)(w + 1) + T) * TT * (int64_t)sizeof(double) + npad * 16;
+    size_t free_b = 0, total_b = 0;
+    HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+    const double avail = 0.9 * (double)free_b;
+    if (avail < (double)ring_wg * 64)
+        throw std::invalid_argument("lsq_cov_band: no device memory left for the sweeps of a " + std::to_string(w) +
+                                    "-tile band");
+    // rings for up to `cap` concurrent workgroups (launches are batched beyond)
+    const int64_t nop_wg = (nops + TB - 1) / TB;
+    const int64_t cap = std::min<int64_t>({(int64_t)(0.5 * avail / ring_wg), std::max(T, nop_wg), 1 << 16});
+    DBuf<double> ring(cap * (w + 1) * TT);
     // the diagonal: identity right-hand sides, tile J from row J on
     DBuf<double> ssq(npad), dE(n);
-    run_sweeps<true>(st, b, T, cap, nullptr, nullptr, nullptr, nullptr, nullptr, sc.p, ring.p, ssq.p);
-    hipLaunchKernelGGL(k_band_diag_sweep, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, dperm.p, ssq.p, sc.p, dE.p);
+    run_sweeps<true>(st, b, T, cap, nullptr, nullptr, nullptr, nullptr, nullptr, F.sc.p, ring.p, ssq.p);
+    hipLaunchKernelGGL(k_band_diag_sweep, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, F.perm.p, ssq.p, F.sc.p, dE.p);
     KERNEL_CHECK();
     dE.download(h_E, n, st);
     HIP_CHECK(hipStreamSynchronize(st));
@@ -526,7 +706,7 @@ void band_cov(System& S, const int32_t* h_perm, double* h_E, int64_t nops, const
         dsegE.upload(so.segE.data(), (int64_t)so.segE.size(), st);
         del.upload(so.el.data(), (int64_t)so.el.size(), st);
         dev.upload(so.ev.data(), (int64_t)so.ev.size(), st);
-        run_sweeps<false>(st, b, nwg, cap, dsp.p, dsegK.p, dsegE.p, del.p, dev.p, sc.p, ring.p, dout.p);
+        run_sweeps<false>(st, b, nwg, cap, dsp.p, dsegK.p, dsegE.p, del.p, dev.p, F.sc.p, ring.p, dout.p);
         std::vector<double> o(nwg * TB);
         dout.download(o.data(), nwg * TB, st);
         HIP_CHECK(hipStreamSynchronize(st));

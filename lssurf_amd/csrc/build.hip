@@ -715,7 +715,8 @@ void scaling_rows_colnorm(System& S, int precond, bool raw) {
     const int64_t m = S.G.m, n = S.G.n;
     hipLaunchKernelGGL(k_rowscale, dim3(grid_for(m)), dim3(BLOCK), 0, st, m, S.roww.p, S.rowkeep.p, S.rs.p);
     KERNEL_CHECK();
-    S.dense_valid = false;   // the dense and block factors depend on the row scaling
+    S.dense_valid = false;   // the dense, band and block factors depend on the row scaling
+    S.band.valid = false;
     S.blk_valid = false;
     if (precond == 1 && S.mf)
         mf_column_scale(S, raw);

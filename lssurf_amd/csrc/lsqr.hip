@@ -428,14 +428,16 @@ void launch_iteration(System& S, const Grids& g, int p, int precond) {
     hipStream_t st = S.stream;
     double* vt = p ? S.vb1.p : S.vb0.p;
     double* vo = p ? S.vb0.p : S.vb1.p;
-    const bool dense = precond == 2, block = precond == 3;
+    const bool dense = precond == 2, block = precond == 3, band = precond == 5;
     if (dense)   // z = R⁻¹ ṽ / α
         hipLaunchKernelGGL(k_gemv_upper, dim3(g.gR), dim3(BLOCK), 0, st, S.dRi.p, S.G.n, S.dense_ld, vt, S.st.p, 1,
                            S.zt.p);
-    // gathered vector: ṽ (values carry cs), R⁻¹ṽ/α (dense), or z = M ṽ from the block epilogue
+    if (band)    // z = M ṽ / α, M = P S R̃⁻¹ (band back substitution)
+        band_launch_bsub(S, vt, 1, S.zt.p);
+    // gathered vector: ṽ (values carry cs), R⁻¹ṽ/α (dense / band), or z = M ṽ from the block epilogue
     hipLaunchKernelGGL(k_xw_spmv, dim3(g.gX + g.gA), dim3(BLOCK), 0, st, S.st.p, g.gX, S.G.n, S.y.p, S.w.p, vt,
-                       (dense || block) ? S.zt.p : vt, dense ? 0 : 1, S.G.m, S.A.nslices, S.A.sp.p, S.A.ci.p,
-                       S.A.val.p, S.u.p, S.part_u.p, S.part_w.p);
+                       (dense || block || band) ? S.zt.p : vt, (dense || band) ? 0 : 1, S.G.m, S.A.nslices, S.A.sp.p,
+                       S.A.ci.p, S.A.val.p, S.u.p, S.part_u.p, S.part_w.p);
     hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gA, S.part_b.p, 0, 0, nullptr);
     if (block) {
         hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, S.G.n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
@@ -448,6 +450,11 @@ void launch_iteration(System& S, const Grids& g, int p, int precond) {
         hipLaunchKernelGGL(k_gemvT_upper, dim3(g.gRT), dim3(BLOCK), 0, st, S.dRi.p, S.G.n, S.dense_ld, S.tt.p, S.st.p,
                            1, vt, vo, S.part_v.p);
         hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gRT, S.part_w.p, g.gX, 0, nullptr);
+    } else if (band) {   // raw Aᵀũ, then ṽ' = Mᵀ t/β − βṽ/α by the band forward substitution
+        hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, S.G.n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
+                           S.AT.val.p, S.u.p, vt, S.tt.p, S.part_v.p, 1);
+        band_launch_fsub(S, S.tt.p, vt, vo, S.part_v.p);
+        hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, 1, S.part_w.p, g.gX, 0, nullptr);
     } else {
         hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, S.G.n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
                            S.AT.val.p, S.u.p, vt, vo, S.part_v.p, 0);
@@ -571,7 +578,7 @@ void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts&
     ensure_workspace(S);
     const Grids g = grids_for(S);
     const int64_t m = S.G.m, n = S.G.n;
-    const bool dense = o.precond == 2, block = o.precond == 3;
+    const bool dense = o.precond == 2, block = o.precond == 3, band = o.precond == 5;
     DBuf<double> db(std::max<int64_t>(m, 1));
     db.upload(h_b, m, st);
     DBuf<double> dx0, dy0;
@@ -585,6 +592,8 @@ void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts&
         } else if (dense) {   // y0 = R x0 ; the SELL values are unscaled, so A·M·y0 = A x0
             hipLaunchKernelGGL(k_gemv_upper, dim3(g.gR), dim3(BLOCK), 0, st, S.dR.p, n, S.dense_ld, dx0.p, nullptr, 2,
                                dy0.p);
+        } else if (band) {    // y0 = M⁻¹ x0 = R̃ S⁻¹ Pᵀ x0
+            band_launch_warm(S, dx0.p, dy0.p);
         } else {       // y0 = x0 / cs ; A·D·y0 = A x0 with the scaled SELL values
             hipLaunchKernelGGL(k_scale, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, dx0.p, S.cs.p, 1, dy0.p);
         }
@@ -599,7 +608,7 @@ void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts&
     h.cs2 = -1.0;
     HIP_CHECK(hipMemcpyAsync(S.st.p, &h, sizeof(h), hipMemcpyHostToDevice, st));
     // the SpMV of the warm start gathers in A·M coordinates: y0 for precond 0/1, x0 for 2 and 3
-    const double* gather0 = h_x0 ? ((dense || block) ? dx0.p : dy0.p) : nullptr;
+    const double* gather0 = h_x0 ? ((dense || block || band) ? dx0.p : dy0.p) : nullptr;
     hipLaunchKernelGGL(k_init_u, dim3(g.gA), dim3(BLOCK), 0, st, m, S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p,
                        S.rs.p, db.p, gather0, S.A.perm.p, S.u.p, S.bw.p, S.part_u.p, S.part_b.p);
     KERNEL_CHECK();
@@ -618,6 +627,11 @@ void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts&
         hipLaunchKernelGGL(k_gemvT_upper, dim3(g.gRT), dim3(BLOCK), 0, st, S.dRi.p, n, S.dense_ld, S.tt.p, S.st.p, 1,
                            S.vb1.p, S.vb0.p, S.part_v.p);
         nv = g.gRT;
+    } else if (band) {
+        hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
+                           S.AT.val.p, S.u.p, S.vb1.p, S.tt.p, S.part_v.p, 1);
+        band_launch_fsub(S, S.tt.p, S.vb1.p, S.vb0.p, S.part_v.p);
+        nv = 1;
     } else {
         hipLaunchKernelGGL(k_spmtv, dim3(g.gT), dim3(BLOCK), 0, st, S.st.p, n, S.AT.nslices, S.AT.sp.p, S.AT.ci.p,
                            S.AT.val.p, S.u.p, S.vb1.p, S.vb0.p, S.part_v.p, 0);
@@ -737,13 +751,16 @@ void fill_stats(const LsqState& h, lsq_stats* s) {
     s->xnorm = h.xnorm;
 }
 
-bool use_mf(const System& S, const lsq_opts& o) { return S.mf && o.op == 0 && o.precond != 2 && !S.dist; }
+bool use_mf(const System& S, const lsq_opts& o) {
+    return S.mf && o.op == 0 && o.precond != 2 && o.precond != 5 && !S.dist;
+}
 
 void prepare(System& S, int precond, bool mf) {
     if (!mf) ensure_sell(S);
     refresh_scaling(S, precond);
     if (precond == 2 && !S.dense_valid) dense_factor(S);
     if (precond == 3 && !S.blk_valid) block_factor(S);
+    if (precond == 5 && !S.band.valid) band_precond(S);
 }
 
 }  // namespace
@@ -790,6 +807,8 @@ int lsqr_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq
     else if (o.precond == 2)
         hipLaunchKernelGGL(k_gemv_upper, dim3(g.gR), dim3(BLOCK), 0, S.stream, S.dRi.p, n, S.dense_ld, S.y.p, nullptr,
                            2, S.vb1.p);
+    else if (o.precond == 5)
+        band_launch_bsub(S, S.y.p, 2, S.vb1.p);
     else
         hipLaunchKernelGGL(k_scale, dim3(grid_for(n)), dim3(BLOCK), 0, S.stream, n, S.y.p, S.cs.p, 0, S.vb1.p);
     KERNEL_CHECK();

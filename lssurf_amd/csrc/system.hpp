@@ -120,6 +120,18 @@ struct LsqState {
     int32_t pad[2];
 };
 
+// Banded Cholesky factor of the equilibrated, permuted normal matrix (band.hip):
+// S Pᵀ(AᵀA)P S = R̃ᵀR̃ with R̃ upper, stored as T tile rows × (w+1) 64×64 tiles (tile (I, J) at
+// (I·(w+1) + J − I)·4096), D_K = R̃_KK⁻¹, sc = the diagonal of S (new order, npad), perm: new
+// position -> compact column.
+struct BandFactor {
+    int64_t n = 0, T = 0;
+    int w = 0;
+    DBuf<double> R, D, sc;
+    DBuf<int32_t> perm;
+    bool valid = false;
+};
+
 // CGNR normal operator (lsqr_cg.inc): AᵀA of the stencil rows of one grid is a constant-coefficient
 // stencil whose coefficients depend only on each node's boundary class (position within K_e of
 // either end of dim e, else interior).  Tiles of CG_TX nodes of dim 1 × ty rows of dim 0 × all of
@@ -264,6 +276,10 @@ struct System {
     int64_t dense_ld = 0;
     bool dense_valid = false;
 
+    // band factor (precond 5, band.hip): AᵀA in the column order band_order (empty = natural)
+    BandFactor band;
+    std::vector<int32_t> band_order;
+
     // distributed layout (y-slab partition, one rank per GPU): columns [0, n_own) are owned,
     // [n_own, G.n) are ghosts grouped by owner; rows are all owned.  One exchange plan serves
     // the forward halo (owned values -> peers' ghost slots) and the reverse halo (ghost partial
@@ -349,6 +365,11 @@ void build_dmf(System& S, int32_t n_grids, const lsq_grid_desc* grids, int32_t n
 void ensure_sell(System& S);                    // assembled A / AT (lazy when S.mf)
 void refresh_scaling(System& S, int precond);
 // band.hip: sqrt(diag((AᵀA)⁻¹)) and op-row variances from a banded Cholesky + Takahashi inverse
+void band_factor(System& S, const int32_t* perm, BandFactor& F);
+void band_precond(System& S);   // S.band from S.band_order (precond 5)
+void band_launch_bsub(System& S, const double* v, int scale_mode, double* out);
+void band_launch_fsub(System& S, const double* t, const double* vin, double* vout, double* part);
+void band_launch_warm(System& S, const double* x0, double* y0);
 void band_cov(System& S, const int32_t* perm, double* E, int64_t nops, const int64_t* rp, const int32_t* ci,
               const double* v, double* op_err, int64_t* info);   // rs/cs -> SELL values (single GPU)
 void scaling_rows_colnorm(System& S, int precond, bool raw);

@@ -225,6 +225,13 @@ class LSQSolver:
         self._check(self._L.lsq_get_rinv(self._h, ptr(Ri)), 'lsq_get_rinv')
         return Ri
 
+    def set_band_order(self, perm=None):
+        """Column order for precond 5 (new position -> compact column; None = natural)."""
+        pp = None if perm is None else as_c(perm, np.int32)
+        n = 0 if pp is None else pp.size
+        self._check(self._L.lsq_set_band_order(self._h, n, ptr(pp) if pp is not None else None),
+                    'lsq_set_band_order')
+
     def cov_band(self, perm=None, op=None):
         """(E, op_err, info) of the current weighted, masked system without a dense factor:
         E = sqrt(diag((AᵀA)⁻¹)) per compact column and, for the rows of `op` (scipy sparse over

@@ -6,13 +6,53 @@ computed by device LSQR to a tight tolerance (atol = btol = 1e-12 by default) in
 sparse QR factorisation.  A full-column-rank A has a unique solution, so results agree with
 SuiteSparseQR to the tolerance in DESIGN.md §Parity.  ``tolerance`` (SPQR's rank tolerance)
 has no LSQR meaning and is ignored.  ``import lssurf_amd.sparseqr_compat as sparseqr``.
+
+Preconditioner (``precond='auto'``): the banded Cholesky factor of AᵀA (precond 5) in the
+natural column order when AᵀA is banded there (lin_op grids are row-major), else in reverse
+Cuthill-McKee order, else column scaling (precond 1) when the band does not fit.  The
+anisotropic notebook system needs > 5·10⁴ column-scaled LSQR iterations; with the band factor a
+handful.
 """
 import numpy as np
 import scipy.sparse as sp
 
+from ._native import NativeError
 from .solver import LSQSolver
 
-_DEFAULTS = dict(atol=1e-12, btol=1e-12, conlim=1e12, precond=1)
+_DEFAULTS = dict(atol=1e-12, btol=1e-12, conlim=1e12, precond='auto')
+BAND_MAX_COLS = 250 * 64     # widest band (columns) precond 5 is tried on
+
+
+def ata_bandwidth(A, perm=None):
+    """Half bandwidth of AᵀA (max |i − j| over its non-zeros) in the column order `perm`
+    (new position -> column; None = natural), from the column span of each row of A."""
+    A = sp.csr_matrix(A)
+    if perm is not None:
+        pos = np.empty(A.shape[1], np.int64)
+        pos[np.asarray(perm)] = np.arange(A.shape[1])
+        cols = pos[A.indices]
+    else:
+        cols = A.indices.astype(np.int64)
+    nz = np.diff(A.indptr) > 0
+    if not nz.any():
+        return 0
+    starts = A.indptr[:-1][nz]
+    hi = np.maximum.reduceat(cols, starts)
+    lo = np.minimum.reduceat(cols, starts)
+    return int((hi - lo).max())
+
+
+def band_order(A):
+    """(perm or None, half bandwidth): natural order when it is banded, else reverse
+    Cuthill-McKee of the pattern of AᵀA."""
+    b = ata_bandwidth(A)
+    if b <= BAND_MAX_COLS:
+        return None, b
+    from scipy.sparse.csgraph import reverse_cuthill_mckee
+    P = sp.csr_matrix(A, dtype=bool).astype(np.float32)
+    N = (P.T @ P).tocsr()
+    perm = np.asarray(reverse_cuthill_mckee(N, symmetric_mode=True), np.int32)
+    return perm, ata_bandwidth(A, perm)
 
 
 def solve(A, b, tolerance=None, device=0, **opts):
@@ -22,9 +62,21 @@ def solve(A, b, tolerance=None, device=0, **opts):
         cols = [solve(A, b[:, k], tolerance, device, **opts) for k in range(b.shape[1])]
         return np.stack(cols, axis=1)
     kw = dict(_DEFAULTS, **opts)
+    auto = kw['precond'] == 'auto'
     with LSQSolver(device) as s:
         s.set_matrix_coo(A.shape[0], A.shape[1], A.row, A.col, A.data)
-        x, stats = s.solve(b, **kw)
+        if auto:
+            perm, bw = band_order(A)
+            kw['precond'] = 5 if bw <= BAND_MAX_COLS else 1
+            if kw['precond'] == 5:
+                s.set_band_order(perm)
+        try:
+            x, stats = s.solve(b, **kw)
+        except NativeError:
+            if not (auto and kw['precond'] == 5):
+                raise
+            kw['precond'] = 1            # the band did not fit the device: column scaling
+            x, stats = s.solve(b, **kw)
     solve.last_stats = stats
     return x
 
