@@ -271,10 +271,37 @@ __global__ __launch_bounds__(TB) void k_band_trsm(BandDev b, int64_t K) {
     for (int i = 0; i < TB; ++i) Nt[i * TB + c] = x[i];
 }
 
-// N_{K+a, K+c} −= R_{K,K+a}ᵀ R_{K,K+c}, 1 ≤ a ≤ c ≤ m (grid m·m, lower pairs idle)
+// R_KJ = D_Kᵀ N_KJ on MFMA (one workgroup per tile): ~10× faster than the substitution but loses
+// ~cond(R_KK)·ε per tile row — used for the preconditioner (precond 5), whose accuracy LSQR
+// absorbs, not for error propagation
+__global__ __launch_bounds__(BLOCK) void k_band_trsm_mfma(BandDev b, int64_t K) {
+    __shared__ double A[TB * LDP];
+    __shared__ double B[TB * LDP];
+    double* Nt = btile(b.R, b.w, K, K + 1 + blockIdx.x);
+    lds_tile<false>(A, b.D + K * TT);
+    lds_tile<false>(B, Nt);
+    __syncthreads();
+    d4 acc[2][2];
+    acc_zero(acc);
+    mma_tile<true>(A, B, acc);
+    acc_each(acc, [&](int r, int c, double v) { Nt[r * TB + c] = v; });
+}
+
+// N_{K+a, K+c} −= R_{K,K+a}ᵀ R_{K,K+c}, 1 ≤ a ≤ c ≤ m, one workgroup per pair.  ROW: only the
+// next tile row (a = 1, c = 1 + blockIdx.x) — the look-ahead the next POTRF/TRSM wait for;
+// otherwise the rest (2 ≤ a ≤ c ≤ m, (m−1)m/2 workgroups), which runs beside them on a second
+// stream.  (A square m² grid with the lower pairs idle cost ~2× in dispatch at w = 65.)
+template <bool ROW>
 __global__ __launch_bounds__(BLOCK) void k_band_syrk(BandDev b, int64_t K, int m) {
-    const int a = blockIdx.x % m + 1, c = blockIdx.x / m + 1;
-    if (a > c) return;
+    int a = 1, c = 1 + (int)blockIdx.x;
+    if (!ROW) {
+        const int p = blockIdx.x;
+        int c0 = (int)((sqrt(8.0 * p + 1.0) - 1.0) * 0.5);
+        while ((c0 + 1) * (c0 + 2) / 2 <= p) ++c0;
+        while (c0 * (c0 + 1) / 2 > p) --c0;
+        a = p - c0 * (c0 + 1) / 2 + 2;
+        c = c0 + 2;
+    }
     __shared__ double A[TB * LDP];
     __shared__ double B[TB * LDP];
     lds_tile<true>(A, btile(b.R, b.w, K, K + a));
@@ -378,26 +405,72 @@ __global__ __launch_bounds__(BLOCK) void k_band_diag_sweep(int64_t n, const int3
 }
 
 // ---- precond 5: LSQR on A·M, M = P·S·R̃⁻¹ (lsqr.hip) ------------------------------------------
-// One workgroup walks the band tile row by tile row (a triangular solve is a chain of T dependent
-// steps); the last w+1 solved tiles stay in an LDS ring, the band tiles stream from HBM with each
-// thread owning a 16-wide segment of one row (bsub) or column (fsub) of every tile.
+// A triangular solve is a chain of T dependent tile steps.  NW workgroups (one per CU, all
+// resident: NW ≤ 64 on a 256-CU device) split each step's w band tiles, publish their partial
+// 64-vectors, meet at a grid barrier, and every workgroup then finishes the step redundantly
+// (sum of the partials in a fixed order, the 64×64 diagonal-block product), keeping the last w+1
+// solved tiles in its own LDS ring.  One barrier per step; the partials are double-buffered by
+// step parity (a workgroup can be at most one barrier ahead).  A single workgroup streamed the
+// band at ~45 GB/s (3 s per solve at 2048²).
+
+struct GridBar {
+    unsigned int count, gen;
+    int err, pad;
+};
+
+// all NW workgroups of the launch meet; false when a barrier timed out (then every workgroup
+// leaves its loop: a bounded spin, so a launch that is not co-resident fails instead of hanging)
+__device__ __forceinline__ bool grid_barrier(GridBar* g, unsigned int nwg, unsigned int& gen) {
+    __shared__ int ok;
+    __threadfence();   // every thread's partial-sum stores, before the workgroup arrives
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ok = 1;
+        __threadfence();
+        const unsigned int arrived = atomicAdd(&g->count, 1u) + 1u;
+        if (arrived == nwg) {
+            atomicExch(&g->count, 0u);
+            __threadfence();
+            atomicAdd(&g->gen, 1u);
+        } else {
+            long spins = 0;
+            while (__hip_atomic_load(&g->gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+                if (++spins > (1L << 24) || __hip_atomic_load(&g->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    atomicExch(&g->err, 1);
+                    ok = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        ++gen;
+    }
+    __syncthreads();
+    return ok != 0;
+}
 
 // out = M·v·scale: x̃ = R̃⁻¹ v by back substitution, x̃_K = D_K (v_K − Σ_{J=K+1}^{K+w} R̃_KJ x̃_J),
 // out[perm[j]] = sc_j x̃_j.  scale_mode 1: v / α (and nothing once the solve stopped), 2: v.
+// Workgroup p takes the tiles J − K − 1 ≡ p (mod NW); thread (r = t/4, q = t%4) a 16-wide
+// segment of row r of each.
 __global__ __launch_bounds__(BLOCK) void k_band_bsub(const double* __restrict__ R, const double* __restrict__ D,
                                                      int64_t T, int w, int64_t n, const double* __restrict__ v,
                                                      const LsqState* __restrict__ st, int scale_mode,
                                                      const double* __restrict__ sc, const int32_t* __restrict__ perm,
-                                                     double* __restrict__ out) {
+                                                     double* __restrict__ out, double* __restrict__ part,
+                                                     GridBar* __restrict__ bar) {
     if (st && st->stop && scale_mode != 2) return;
     extern __shared__ double ring[];   // (w+1) × 64
     __shared__ double Y[TB];
+    const unsigned int NW = gridDim.x, p = blockIdx.x;
+    unsigned int gen = 0;
     const double scale = scale_mode == 1 ? st->inv_alpha : 1.0;
     const int t = threadIdx.x, r = t >> 2, q = t & 3;
     for (int64_t K = T - 1; K >= 0; --K) {
         double acc = 0.0;
         const int64_t J1 = min<int64_t>(K + w, T - 1);
-        for (int64_t J = K + 1; J <= J1; ++J) {
+        for (int64_t J = K + 1 + p; J <= J1; J += NW) {
             const double2* Rt = reinterpret_cast<const double2*>(R + ((K * (w + 1)) + (J - K)) * TT + r * TB + q * 16);
             const double* xs = ring + (J % (w + 1)) * TB + q * 16;
 #pragma unroll
@@ -408,8 +481,15 @@ __global__ __launch_bounds__(BLOCK) void k_band_bsub(const double* __restrict__ 
         }
         acc += __shfl_xor(acc, 1);
         acc += __shfl_xor(acc, 2);
+        double* pb = part + (K & 1) * NW * TB;
+        if (q == 0) pb[p * TB + r] = acc;
+        if (NW > 1 && !grid_barrier(bar, NW, gen)) return;
         const int64_t j = K * TB + r;
-        if (q == 0) Y[r] = (j < n ? v[j] * scale : 0.0) - acc;
+        if (q == 0) {
+            double s = 0.0;
+            for (unsigned int pp = 0; pp < NW; ++pp) s += pb[pp * TB + r];
+            Y[r] = (j < n ? v[j] * scale : 0.0) - s;
+        }
         __syncthreads();
         const double* Dr = D + K * TT + r * TB + q * 16;   // x̃_K = D_K Y (D upper)
         double x = 0.0;
@@ -419,7 +499,7 @@ __global__ __launch_bounds__(BLOCK) void k_band_bsub(const double* __restrict__ 
         x += __shfl_xor(x, 2);
         if (q == 0) {
             ring[(K % (w + 1)) * TB + r] = x;
-            if (j < n) out[perm[j]] = sc[j] * x;
+            if (p == 0 && j < n) out[perm[j]] = sc[j] * x;
         }
         __syncthreads();
     }
@@ -427,22 +507,26 @@ __global__ __launch_bounds__(BLOCK) void k_band_bsub(const double* __restrict__ 
 
 // vout = R̃⁻ᵀ (S Pᵀ t) with LSQR's epilogue (as dense.hip's k_gemvT_upper mode 1):
 // ỹ_K = D_Kᵀ (t̃_K − Σ_{I=K−w}^{K−1} R̃_IKᵀ ỹ_I), vout_j = ỹ_j/β − β vin_j/α (vin_j when β = 0),
-// part[0] = Σ vout².
+// part[0] = Σ vout².  Workgroup p takes the tiles K − 1 − I ≡ p (mod NW); thread (c = t%64,
+// q = t/64) rows q·16 .. q·16+15 of column c of each.
 __global__ __launch_bounds__(BLOCK) void k_band_fsub(const double* __restrict__ R, const double* __restrict__ D,
                                                      int64_t T, int w, int64_t n, const double* __restrict__ tin,
                                                      const LsqState* __restrict__ st, const double* __restrict__ vin,
                                                      double* __restrict__ vout, const double* __restrict__ sc,
-                                                     const int32_t* __restrict__ perm, double* __restrict__ part) {
+                                                     const int32_t* __restrict__ perm, double* __restrict__ part,
+                                                     double* __restrict__ pv, GridBar* __restrict__ bar) {
     if (st && st->stop) return;
     extern __shared__ double ring[];   // (w+1) × 64
     __shared__ double Z[TB];
     __shared__ double P4[4][TB];
     __shared__ double red[4];
-    const int t = threadIdx.x, c = t & 63, q = t >> 6;   // column c, rows q*16 .. q*16+15
+    const unsigned int NW = gridDim.x, p = blockIdx.x;
+    unsigned int gen = 0;
+    const int t = threadIdx.x, c = t & 63, q = t >> 6;
     double sv = 0.0;
     for (int64_t K = 0; K < T; ++K) {
         double acc = 0.0;
-        for (int64_t I = max<int64_t>(0, K - w); I < K; ++I) {
+        for (int64_t I = K - 1 - p; I >= max<int64_t>(0, K - w); I -= NW) {
             const double* Rt = R + ((I * (w + 1)) + (K - I)) * TT + (q * 16) * TB + c;
             const double* ys = ring + (I % (w + 1)) * TB + q * 16;
 #pragma unroll
@@ -450,8 +534,15 @@ __global__ __launch_bounds__(BLOCK) void k_band_fsub(const double* __restrict__ 
         }
         P4[q][c] = acc;
         __syncthreads();
+        double* pb = part + (K & 1) * NW * TB;
+        if (q == 0) pb[p * TB + c] = (P4[0][c] + P4[1][c]) + (P4[2][c] + P4[3][c]);
+        if (NW > 1 && !grid_barrier(bar, NW, gen)) return;
         const int64_t j = K * TB + c;
-        if (q == 0) Z[c] = (j < n ? tin[perm[j]] * sc[j] : 0.0) - ((P4[0][c] + P4[1][c]) + (P4[2][c] + P4[3][c]));
+        if (q == 0) {
+            double s = 0.0;
+            for (unsigned int pp = 0; pp < NW; ++pp) s += pb[pp * TB + c];
+            Z[c] = (j < n ? tin[perm[j]] * sc[j] : 0.0) - s;
+        }
         __syncthreads();
         const double* Dc = D + K * TT + (q * 16) * TB + c;   // (D_Kᵀ Z)_c = Σ_r D[r][c] Z[r]
         double y = 0.0;
@@ -462,7 +553,7 @@ __global__ __launch_bounds__(BLOCK) void k_band_fsub(const double* __restrict__ 
         if (q == 0) {
             const double yc = (P4[0][c] + P4[1][c]) + (P4[2][c] + P4[3][c]);
             ring[(K % (w + 1)) * TB + c] = yc;
-            if (j < n) {
+            if (p == 0 && j < n) {
                 const double o = st->skip_v ? vin[j] : yc * st->inv_beta - st->beta * (vin[j] * st->inv_alpha);
                 vout[j] = o;
                 sv += o * o;
@@ -471,7 +562,7 @@ __global__ __launch_bounds__(BLOCK) void k_band_fsub(const double* __restrict__ 
         __syncthreads();
     }
     const double s = block_sum(sv, red);
-    if (threadIdx.x == 0) part[0] = s;
+    if (p == 0 && threadIdx.x == 0) pv[0] = s;
 }
 
 // warm start y0 = M⁻¹ x0 = R̃ S⁻¹ Pᵀ x0 (one thread per row of R̃)
@@ -554,7 +645,7 @@ void run_sweeps(hipStream_t st, const BandDev& b, int64_t nwg, int64_t cap, cons
 
 // AᵀA of the current weighted, masked system in the order h_perm (nullable: natural), equilibrated
 // and factored inside its band into F
-void band_factor(System& S, const int32_t* h_perm, BandFactor& F) {
+void band_factor(System& S, const int32_t* h_perm, BandFactor& F, bool fast_trsm) {
     hipStream_t st = S.stream;
     const int64_t n = S.G.n;
     if (n <= 0) throw std::invalid_argument("band factor: empty system");
@@ -604,14 +695,31 @@ void band_factor(System& S, const int32_t* h_perm, BandFactor& F) {
     KERNEL_CHECK();
     DBuf<int> err(1);
     err.zero(st);
+    if (!S.side) {
+        HIP_CHECK(hipStreamCreateWithFlags(&S.side, hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&S.ev_fork, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&S.ev_join, hipEventDisableTiming));
+    }
+    // look-ahead: step K's POTRF, TRSM and next-row update on the main stream; the rest of its
+    // trailing update (rows K+2..) on the side stream, joined before the next-row update of K+1
+    HIP_CHECK(hipEventRecord(S.ev_join, st));
     for (int64_t K = 0; K < T; ++K) {
         hipLaunchKernelGGL(k_band_potrf, dim3(1), dim3(TB), 0, st, b, K, err.p);
         const int m = (int)std::min<int64_t>(w, T - 1 - K);
         if (m > 0) {
-            hipLaunchKernelGGL(k_band_trsm, dim3(m), dim3(TB), 0, st, b, K);
-            hipLaunchKernelGGL(k_band_syrk, dim3(m * m), dim3(BLOCK), 0, st, b, K, m);
+            if (fast_trsm) hipLaunchKernelGGL(k_band_trsm_mfma, dim3(m), dim3(BLOCK), 0, st, b, K);
+            else hipLaunchKernelGGL(k_band_trsm, dim3(m), dim3(TB), 0, st, b, K);
+            HIP_CHECK(hipStreamWaitEvent(st, S.ev_join, 0));
+            hipLaunchKernelGGL(k_band_syrk<true>, dim3(m), dim3(BLOCK), 0, st, b, K, m);
+            if (m > 1) {
+                HIP_CHECK(hipEventRecord(S.ev_fork, st));
+                HIP_CHECK(hipStreamWaitEvent(S.side, S.ev_fork, 0));
+                hipLaunchKernelGGL(k_band_syrk<false>, dim3((m - 1) * m / 2), dim3(BLOCK), 0, S.side, b, K, m);
+                HIP_CHECK(hipEventRecord(S.ev_join, S.side));
+            }
         }
     }
+    HIP_CHECK(hipStreamWaitEvent(st, S.ev_join, 0));
     KERNEL_CHECK();
     int h_err = 0;
     HIP_CHECK(hipMemcpyAsync(&h_err, err.p, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -624,7 +732,7 @@ void band_factor(System& S, const int32_t* h_perm, BandFactor& F) {
 constexpr int BAND_PRECOND_WMAX = 300;
 
 void band_precond(System& S) {
-    band_factor(S, S.band_order.empty() ? nullptr : S.band_order.data(), S.band);
+    band_factor(S, S.band_order.empty() ? nullptr : S.band_order.data(), S.band, true);
     if (S.band.w > BAND_PRECOND_WMAX) {
         S.band.valid = false;
         throw std::invalid_argument("precond 5: the band of AᵀA is " + std::to_string(S.band.w) +
@@ -633,16 +741,50 @@ void band_precond(System& S) {
     }
 }
 
+// workgroups of the multi-workgroup triangular solves (≤ 64: co-resident on any 256-CU device)
+int band_nw(const BandFactor& F) { return std::max(1, std::min(F.w, 64)); }
+
+void band_solve_scratch(System& S) {
+    BandFactor& F = S.band;
+    const int nw = band_nw(F);
+    if (F.part.n < 2 * nw * TB) F.part.alloc(2 * nw * TB);
+    if (!F.bar.p) {
+        F.bar.alloc(2);
+        F.bar.zero(S.stream);
+    }
+}
+
+// a multi-workgroup solve whose barrier timed out (workgroups not co-resident) leaves err set in
+// the barrier (only count / gen are reset per launch): fail loudly instead of returning garbage
+void band_check(System& S) {
+    if (!S.band.bar.p) return;
+    GridBar h{};
+    HIP_CHECK(hipMemcpyAsync(&h, S.band.bar.p, sizeof(h), hipMemcpyDeviceToHost, S.stream));
+    HIP_CHECK(hipStreamSynchronize(S.stream));
+    if (h.err) {
+        S.band.bar.zero(S.stream);
+        throw std::runtime_error("precond 5: a band triangular solve's grid barrier timed out");
+    }
+}
+
 void band_launch_bsub(System& S, const double* v, int scale_mode, double* out) {
-    const BandFactor& F = S.band;
-    hipLaunchKernelGGL(k_band_bsub, dim3(1), dim3(BLOCK), sizeof(double) * TB * (F.w + 1), S.stream, F.R.p, F.D.p, F.T,
-                       F.w, F.n, v, S.st.p, scale_mode, F.sc.p, F.perm.p, out);
+    BandFactor& F = S.band;
+    band_solve_scratch(S);
+    const int nw = band_nw(F);
+    HIP_CHECK(hipMemsetAsync(F.bar.p, 0, 2 * sizeof(unsigned int), S.stream));   // count, gen (err is sticky)
+    hipLaunchKernelGGL(k_band_bsub, dim3(nw), dim3(BLOCK), sizeof(double) * TB * (F.w + 1), S.stream, F.R.p, F.D.p,
+                       F.T, F.w, F.n, v, S.st.p, scale_mode, F.sc.p, F.perm.p, out, F.part.p,
+                       reinterpret_cast<GridBar*>(F.bar.p));
 }
 
 void band_launch_fsub(System& S, const double* t, const double* vin, double* vout, double* part) {
-    const BandFactor& F = S.band;
-    hipLaunchKernelGGL(k_band_fsub, dim3(1), dim3(BLOCK), sizeof(double) * TB * (F.w + 1), S.stream, F.R.p, F.D.p, F.T,
-                       F.w, F.n, t, S.st.p, vin, vout, F.sc.p, F.perm.p, part);
+    BandFactor& F = S.band;
+    band_solve_scratch(S);
+    const int nw = band_nw(F);
+    HIP_CHECK(hipMemsetAsync(F.bar.p, 0, 2 * sizeof(unsigned int), S.stream));   // count, gen (err is sticky)
+    hipLaunchKernelGGL(k_band_fsub, dim3(nw), dim3(BLOCK), sizeof(double) * TB * (F.w + 1), S.stream, F.R.p, F.D.p,
+                       F.T, F.w, F.n, t, S.st.p, vin, vout, F.sc.p, F.perm.p, F.part.p, part,
+                       reinterpret_cast<GridBar*>(F.bar.p));
 }
 
 void band_launch_warm(System& S, const double* x0, double* y0) {
@@ -660,7 +802,7 @@ void band_cov(System& S, const int32_t* h_perm, double* h_E, int64_t nops, const
         for (int64_t e = h_rp[i]; e < h_rp[i + 1]; ++e)
             if (h_ci[e] < 0 || h_ci[e] >= n) throw std::invalid_argument("lsq_cov_band: op column out of range");
     BandFactor F;
-    band_factor(S, h_perm, F);
+    band_factor(S, h_perm, F, false);
     const int64_t T = F.T, npad = T * TB;
     const int w = F.w;
     std::vector<int32_t> pinv(n);

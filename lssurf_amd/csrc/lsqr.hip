@@ -815,6 +815,7 @@ int lsqr_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq
     S.vb1.download(h_x, n, S.stream);
     HIP_CHECK(hipMemcpyAsync(&h, S.st.p, sizeof(h), hipMemcpyDeviceToHost, S.stream));
     HIP_CHECK(hipStreamSynchronize(S.stream));
+    if (o.precond == 5) band_check(S);
     float ms = 0.f;
     HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
     (void)hipEventDestroy(e0);

@@ -129,6 +129,8 @@ struct BandFactor {
     int w = 0;
     DBuf<double> R, D, sc;
     DBuf<int32_t> perm;
+    DBuf<double> part;         // multi-workgroup triangular solves: partial sums (2 × NW × 64)
+    DBuf<uint64_t> bar;        // and their grid barrier
     bool valid = false;
 };
 
@@ -365,11 +367,12 @@ void build_dmf(System& S, int32_t n_grids, const lsq_grid_desc* grids, int32_t n
 void ensure_sell(System& S);                    // assembled A / AT (lazy when S.mf)
 void refresh_scaling(System& S, int precond);
 // band.hip: sqrt(diag((AᵀA)⁻¹)) and op-row variances from a banded Cholesky + Takahashi inverse
-void band_factor(System& S, const int32_t* perm, BandFactor& F);
+void band_factor(System& S, const int32_t* perm, BandFactor& F, bool fast_trsm);
 void band_precond(System& S);   // S.band from S.band_order (precond 5)
 void band_launch_bsub(System& S, const double* v, int scale_mode, double* out);
 void band_launch_fsub(System& S, const double* t, const double* vin, double* vout, double* part);
 void band_launch_warm(System& S, const double* x0, double* y0);
+void band_check(System& S);   // throws when a precond-5 solve's grid barrier timed out
 void band_cov(System& S, const int32_t* perm, double* E, int64_t nops, const int64_t* rp, const int32_t* ci,
               const double* v, double* op_err, int64_t* info);   // rs/cs -> SELL values (single GPU)
 void scaling_rows_colnorm(System& S, int precond, bool raw);
