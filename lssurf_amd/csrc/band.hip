@@ -205,32 +205,93 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// POTRF of tile (K, K) and D_K = R_KK⁻¹ by ONE wave, lane k holding column k of the tile in
-// registers: no barriers, row j of R broadcast lane by lane with readlane.  Measured per tile:
-// 77 µs (the 256-thread LDS version with 192 barriers: 128 µs; LDS broadcasts within one wave:
-// 140 µs).  The lower triangle is zeroed.
-__global__ __launch_bounds__(TB) void k_band_potrf(BandDev b, int64_t K, int* err) {
-    const int k = threadIdx.x;
+// POTRF of tile (K, K), blocked by 16: per 16-column block, the 16×16 diagonal Cholesky by one
+// wave (columns in registers, rows broadcast with readlane), the 16-row panel by substitution (a
+// thread per trailing column), the trailing triangle's rank-16 update by all 256 threads — 12
+// barriers.  (Unblocked: one wave with readlane, 68 µs per tile; 256 threads with a barrier per
+// elimination step, 128 µs.)  The lower triangle is zeroed.
+__global__ __launch_bounds__(BLOCK) void k_band_potrf(BandDev b, int64_t K, int* err) {
+    __shared__ double A[TB * LDP];
+    __shared__ double rinv[TB];
+    __shared__ int bad;
     double* Rt = btile(b.R, b.w, K, K);
+    for (int idx = threadIdx.x; idx < TT; idx += BLOCK) {
+        const int r = idx >> 6, c = idx & 63;
+        A[r * LDP + c] = c >= r ? Rt[idx] : 0.0;
+    }
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int o = 0; o < TB; o += 16) {
+        if (wv == 0) {   // 16×16 diagonal block: lane k < 16 holds its column o + k
+            double a[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) a[i] = (lane < 16 && i <= lane) ? A[(o + i) * LDP + o + lane] : 0.0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const double d = readlane_d(a[j], j);
+                double r = 1.0;
+                if (d > 0.0) r = sqrt(d);
+                else if (lane == 0) bad = 1;
+                a[j] = lane == j ? r : (lane > j ? a[j] / r : 0.0);
+#pragma unroll
+                for (int i = j + 1; i < 16; ++i) {
+                    const double rji = readlane_d(a[j], i);
+                    if (lane >= i) a[i] -= rji * a[j];
+                }
+            }
+            if (lane < 16) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) A[(o + i) * LDP + o + lane] = i <= lane ? a[i] : 0.0;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < 16) rinv[o + threadIdx.x] = 1.0 / A[(o + threadIdx.x) * LDP + o + threadIdx.x];
+        const int c0 = o + 16, nc = TB - c0;
+        if (nc == 0) break;
+        __syncthreads();
+        if (threadIdx.x < nc) {   // panel: rows o..o+15 of column c, R_bbᵀ X = A by substitution
+            const int c = c0 + threadIdx.x;
+            double x[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x[i] = A[(o + i) * LDP + c];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                x[i] *= rinv[o + i];
+#pragma unroll
+                for (int q = i + 1; q < 16; ++q) x[q] -= A[(o + i) * LDP + o + q] * x[i];
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) A[(o + i) * LDP + c] = x[i];
+        }
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < nc * nc; idx += BLOCK) {   // trailing: A_ic −= Σ_p P_pi P_pc
+            const int i = c0 + idx / nc, c = c0 + idx % nc;
+            if (c < i) continue;
+            double sum = 0.0;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) sum += A[(o + q) * LDP + i] * A[(o + q) * LDP + c];
+            A[i * LDP + c] -= sum;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && bad) atomicExch(err, 1);
+    for (int idx = threadIdx.x; idx < TT; idx += BLOCK) {
+        const int r = idx >> 6, c = idx & 63;
+        Rt[idx] = c >= r ? A[r * LDP + c] : 0.0;
+    }
+}
+
+// D_K = R_KK⁻¹ for every tile row at once (one wave per tile, lane k: column k by back
+// substitution, R's rows broadcast with readlane)
+__global__ __launch_bounds__(TB) void k_band_dinv(BandDev b) {
+    const int64_t K = blockIdx.x;
+    const int k = threadIdx.x;
+    const double* Rt = btile(b.R, b.w, K, K);
     double a[TB];
 #pragma unroll
-    for (int i = 0; i < TB; ++i) a[i] = i <= k ? Rt[i * TB + k] : 0.0;
-    bool bad = false;
-#pragma unroll
-    for (int j = 0; j < TB; ++j) {
-        const double d = readlane_d(a[j], j);
-        double r = 1.0;
-        if (d > 0.0) r = sqrt(d);
-        else bad = true;
-        a[j] = k == j ? r : (k > j ? a[j] / r : 0.0);   // row j of R (column k's entry)
-#pragma unroll
-        for (int i = j + 1; i < TB; ++i) {
-            const double rji = readlane_d(a[j], i);
-            if (k >= i) a[i] -= rji * a[j];
-        }
-    }
-    if (bad && k == 0) atomicExch(err, 1);
-    double x[TB];   // column k of D = R⁻¹: R x = e_k by back substitution
+    for (int i = 0; i < TB; ++i) a[i] = Rt[i * TB + k];   // column k of R (zero below the diagonal)
+    double x[TB];
 #pragma unroll
     for (int i = TB - 1; i >= 0; --i) {
         double s = i == k ? 1.0 : 0.0;
@@ -240,51 +301,54 @@ __global__ __launch_bounds__(TB) void k_band_potrf(BandDev b, int64_t K, int* er
     }
     double* Dk = b.D + K * TT;
 #pragma unroll
-    for (int i = 0; i < TB; ++i) {
-        Rt[i * TB + k] = a[i];
-        Dk[i * TB + k] = x[i];
-    }
+    for (int i = 0; i < TB; ++i) Dk[i * TB + k] = x[i];
 }
 
-// R_KJ = R_KK⁻ᵀ N_KJ for J = K+1..K+m (one wave per tile, lane c holding column c of the tile
-// in registers) by forward substitution with R_KK broadcast from LDS.  Multiplying by the
-// explicit D_Kᵀ instead would lose ~cond(R_KK)·ε per tile row.
-__global__ __launch_bounds__(TB) void k_band_trsm(BandDev b, int64_t K) {
-    __shared__ double R[TT];
-    __shared__ double rdiag[TB];
-    const int c = threadIdx.x;
+// R_KJ = R_KK⁻ᵀ N_KJ for J = K+1..K+m (one workgroup per tile), blocked by 16 rows: the 16 rows
+// of a block by substitution (a thread per column), then the rows below updated with them by all
+// 256 threads — 8 barriers.  Multiplying by the explicit D_Kᵀ instead would lose ~cond(R_KK)·ε
+// per tile row.
+__global__ __launch_bounds__(BLOCK) void k_band_trsm(BandDev b, int64_t K) {
+    __shared__ double R[TB * LDP];
+    __shared__ double X[TB * LDP];
+    __shared__ double rinv[TB];
     const double* Rkk = btile(b.R, b.w, K, K);
-    for (int idx = c; idx < TT; idx += TB) R[idx] = Rkk[idx];
-    rdiag[c] = b.D[K * TT + c * TB + c];   // 1/R_cc (D_K's diagonal, one correctly rounded division)
     double* Nt = btile(b.R, b.w, K, K + 1 + blockIdx.x);
-    double x[TB];
-#pragma unroll
-    for (int i = 0; i < TB; ++i) x[i] = Nt[i * TB + c];
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < TB; ++i) {
-        x[i] *= rdiag[i];
-#pragma unroll
-        for (int p = i + 1; p < TB; ++p) x[p] -= R[i * TB + p] * x[i];
+    for (int idx = threadIdx.x; idx < TT; idx += BLOCK) {
+        const int r = idx >> 6, c = idx & 63;
+        R[r * LDP + c] = Rkk[idx];
+        X[r * LDP + c] = Nt[idx];
     }
-#pragma unroll
-    for (int i = 0; i < TB; ++i) Nt[i * TB + c] = x[i];
-}
-
-// R_KJ = D_Kᵀ N_KJ on MFMA (one workgroup per tile): ~10× faster than the substitution but loses
-// ~cond(R_KK)·ε per tile row — used for the preconditioner (precond 5), whose accuracy LSQR
-// absorbs, not for error propagation
-__global__ __launch_bounds__(BLOCK) void k_band_trsm_mfma(BandDev b, int64_t K) {
-    __shared__ double A[TB * LDP];
-    __shared__ double B[TB * LDP];
-    double* Nt = btile(b.R, b.w, K, K + 1 + blockIdx.x);
-    lds_tile<false>(A, b.D + K * TT);
-    lds_tile<false>(B, Nt);
     __syncthreads();
-    d4 acc[2][2];
-    acc_zero(acc);
-    mma_tile<true>(A, B, acc);
-    acc_each(acc, [&](int r, int c, double v) { Nt[r * TB + c] = v; });
+    if (threadIdx.x < TB) rinv[threadIdx.x] = 1.0 / R[threadIdx.x * LDP + threadIdx.x];
+    __syncthreads();
+    for (int o = 0; o < TB; o += 16) {
+        if (threadIdx.x < TB) {
+            const int c = threadIdx.x;
+            double x[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x[i] = X[(o + i) * LDP + c];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                x[i] *= rinv[o + i];
+#pragma unroll
+                for (int q = i + 1; q < 16; ++q) x[q] -= R[(o + i) * LDP + o + q] * x[i];
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) X[(o + i) * LDP + c] = x[i];
+        }
+        __syncthreads();
+        const int r0 = o + 16, nr = TB - r0;
+        for (int idx = threadIdx.x; idx < nr * TB; idx += BLOCK) {   // X_pc −= Σ_i R_ip X_ic
+            const int pr = r0 + (idx >> 6), c = idx & 63;
+            double sum = 0.0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) sum += R[(o + i) * LDP + pr] * X[(o + i) * LDP + c];
+            X[pr * LDP + c] -= sum;
+        }
+        __syncthreads();
+    }
+    for (int idx = threadIdx.x; idx < TT; idx += BLOCK) Nt[idx] = X[(idx >> 6) * LDP + (idx & 63)];
 }
 
 // N_{K+a, K+c} −= R_{K,K+a}ᵀ R_{K,K+c}, 1 ≤ a ≤ c ≤ m, one workgroup per pair.  ROW: only the
@@ -304,12 +368,13 @@ __global__ __launch_bounds__(BLOCK) void k_band_syrk(BandDev b, int64_t K, int m
     }
     __shared__ double A[TB * LDP];
     __shared__ double B[TB * LDP];
-    lds_tile<true>(A, btile(b.R, b.w, K, K + a));
-    lds_tile<false>(B, btile(b.R, b.w, K, K + c));
+    TilePair tp;   // both tiles' loads in flight together; A used transposed in place (no LDS transpose)
+    tp.load(btile(b.R, b.w, K, K + a), btile(b.R, b.w, K, K + c));
+    tp.store(A, B);
     __syncthreads();
     d4 acc[2][2];
     acc_zero(acc);
-    mma_tile(A, B, acc);
+    mma_tile<true>(A, B, acc);
     double* Ct = btile(b.R, b.w, K + a, K + c);
     acc_each(acc, [&](int r, int cc, double v) { Ct[r * TB + cc] -= v; });
 }
@@ -645,7 +710,7 @@ void run_sweeps(hipStream_t st, const BandDev& b, int64_t nwg, int64_t cap, cons
 
 // AᵀA of the current weighted, masked system in the order h_perm (nullable: natural), equilibrated
 // and factored inside its band into F
-void band_factor(System& S, const int32_t* h_perm, BandFactor& F, bool fast_trsm) {
+void band_factor(System& S, const int32_t* h_perm, BandFactor& F) {
     hipStream_t st = S.stream;
     const int64_t n = S.G.n;
     if (n <= 0) throw std::invalid_argument("band factor: empty system");
@@ -704,11 +769,10 @@ void band_factor(System& S, const int32_t* h_perm, BandFactor& F, bool fast_trsm
     // trailing update (rows K+2..) on the side stream, joined before the next-row update of K+1
     HIP_CHECK(hipEventRecord(S.ev_join, st));
     for (int64_t K = 0; K < T; ++K) {
-        hipLaunchKernelGGL(k_band_potrf, dim3(1), dim3(TB), 0, st, b, K, err.p);
+        hipLaunchKernelGGL(k_band_potrf, dim3(1), dim3(BLOCK), 0, st, b, K, err.p);
         const int m = (int)std::min<int64_t>(w, T - 1 - K);
         if (m > 0) {
-            if (fast_trsm) hipLaunchKernelGGL(k_band_trsm_mfma, dim3(m), dim3(BLOCK), 0, st, b, K);
-            else hipLaunchKernelGGL(k_band_trsm, dim3(m), dim3(TB), 0, st, b, K);
+            hipLaunchKernelGGL(k_band_trsm, dim3(m), dim3(BLOCK), 0, st, b, K);
             HIP_CHECK(hipStreamWaitEvent(st, S.ev_join, 0));
             hipLaunchKernelGGL(k_band_syrk<true>, dim3(m), dim3(BLOCK), 0, st, b, K, m);
             if (m > 1) {
@@ -720,6 +784,7 @@ void band_factor(System& S, const int32_t* h_perm, BandFactor& F, bool fast_trsm
         }
     }
     HIP_CHECK(hipStreamWaitEvent(st, S.ev_join, 0));
+    hipLaunchKernelGGL(k_band_dinv, dim3((unsigned)T), dim3(TB), 0, st, b);
     KERNEL_CHECK();
     int h_err = 0;
     HIP_CHECK(hipMemcpyAsync(&h_err, err.p, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -732,7 +797,7 @@ void band_factor(System& S, const int32_t* h_perm, BandFactor& F, bool fast_trsm
 constexpr int BAND_PRECOND_WMAX = 300;
 
 void band_precond(System& S) {
-    band_factor(S, S.band_order.empty() ? nullptr : S.band_order.data(), S.band, true);
+    band_factor(S, S.band_order.empty() ? nullptr : S.band_order.data(), S.band);
     if (S.band.w > BAND_PRECOND_WMAX) {
         S.band.valid = false;
         throw std::invalid_argument("precond 5: the band of AᵀA is " + std::to_string(S.band.w) +
@@ -802,7 +867,7 @@ void band_cov(System& S, const int32_t* h_perm, double* h_E, int64_t nops, const
         for (int64_t e = h_rp[i]; e < h_rp[i + 1]; ++e)
             if (h_ci[e] < 0 || h_ci[e] >= n) throw std::invalid_argument("lsq_cov_band: op column out of range");
     BandFactor F;
-    band_factor(S, h_perm, F, false);
+    band_factor(S, h_perm, F);
     const int64_t T = F.T, npad = T * TB;
     const int w = F.w;
     std::vector<int32_t> pinv(n);

@@ -367,7 +367,7 @@ void build_dmf(System& S, int32_t n_grids, const lsq_grid_desc* grids, int32_t n
 void ensure_sell(System& S);                    // assembled A / AT (lazy when S.mf)
 void refresh_scaling(System& S, int precond);
 // band.hip: sqrt(diag((AᵀA)⁻¹)) and op-row variances from a banded Cholesky + Takahashi inverse
-void band_factor(System& S, const int32_t* perm, BandFactor& F, bool fast_trsm);
+void band_factor(System& S, const int32_t* perm, BandFactor& F);
 void band_precond(System& S);   // S.band from S.band_order (precond 5)
 void band_launch_bsub(System& S, const double* v, int scale_mode, double* out);
 void band_launch_fsub(System& S, const double* t, const double* vin, double* vout, double* part);

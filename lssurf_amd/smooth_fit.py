@@ -392,9 +392,11 @@ def smooth_fit(**kwargs):
     if args['VERBOSE']:
         print(f"smooth_fit: E_RMS={args['E_RMS']}")
     setup_smoothness_constraints(grids, constraint_op_list, args['E_RMS'], args['mask_scale'])
+    zero_prior = set()   # priors created here are zeros: rhs is already zero on their rows
     for op in constraint_op_list:
         if op.prior is None:
             op.prior = np.zeros_like(op.expected)
+            zero_prior.add(op.name)
     Gc = lin_op(None, name='constraints').vstack(constraint_op_list)
     N_eq = G_data.N_eq + Gc.N_eq
     Ec = np.zeros(Gc.N_eq)
@@ -410,7 +412,13 @@ def smooth_fit(**kwargs):
     TCinv_diag = 1. / np.concatenate((Ed, Ec))
     rhs = np.zeros([N_eq])
     rhs[0:data.size] = data.z.ravel()
-    rhs[data.size:] = np.concatenate([op.prior for op in constraint_op_list])
+    for op in constraint_op_list:   # rhs[data.size:] = the concatenated priors
+        if op.name not in zero_prior:
+            rows = _as_slice(Gc.TOC['rows'][op.name])
+            if isinstance(rows, slice):
+                rhs[data.size + rows.start:data.size + rows.stop] = np.ravel(op.prior)
+            else:
+                rhs[data.size + rows] = np.ravel(op.prior)
     keep_cols = reference_epoch_keep_cols(G_data.col_N, grids['dz'], args['reference_epoch'])
     timing['setup'] = time() - tic
     in_TSE = data.three_sigma_edit > 0.01 if 'three_sigma_edit' in data.fields else np.ones(G_data.N_eq, dtype=bool)
