@@ -518,7 +518,8 @@ __device__ __forceinline__ bool grid_barrier(GridBar* g, unsigned int nwg, unsig
 // out = M·v·scale: x̃ = R̃⁻¹ v by back substitution, x̃_K = D_K (v_K − Σ_{J=K+1}^{K+w} R̃_KJ x̃_J),
 // out[perm[j]] = sc_j x̃_j.  scale_mode 1: v / α (and nothing once the solve stopped), 2: v.
 // Workgroup p takes the tiles J − K − 1 ≡ p (mod NW); thread (r = t/4, q = t%4) a 16-wide
-// segment of row r of each.
+// segment of row r of each.  The next step's first tile and D_K segment are loaded before the
+// barrier (they do not depend on x), so their latency hides behind it.
 __global__ __launch_bounds__(BLOCK) void k_band_bsub(const double* __restrict__ R, const double* __restrict__ D,
                                                      int64_t T, int w, int64_t n, const double* __restrict__ v,
                                                      const LsqState* __restrict__ st, int scale_mode,
@@ -532,10 +533,28 @@ __global__ __launch_bounds__(BLOCK) void k_band_bsub(const double* __restrict__ 
     unsigned int gen = 0;
     const double scale = scale_mode == 1 ? st->inv_alpha : 1.0;
     const int t = threadIdx.x, r = t >> 2, q = t & 3;
+    double2 rn[8];   // row segment of the next step's first tile (zeros when there is none)
+    double dn[16];   // row segment of the next step's D
+    auto fetch = [&](int64_t K) {
+        const int64_t J = K + 1 + p;
+        const bool has = K >= 0 && J <= min<int64_t>(K + w, T - 1);
+        const double2* Rt = reinterpret_cast<const double2*>(R + ((K * (w + 1)) + (J - K)) * TT + r * TB + q * 16);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) rn[c] = has ? Rt[c] : make_double2(0.0, 0.0);
+        const double* Dr = D + (K >= 0 ? K : 0) * TT + r * TB + q * 16;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) dn[c] = K >= 0 ? Dr[c] : 0.0;
+    };
+    fetch(T - 1);
     for (int64_t K = T - 1; K >= 0; --K) {
         double acc = 0.0;
         const int64_t J1 = min<int64_t>(K + w, T - 1);
-        for (int64_t J = K + 1 + p; J <= J1; J += NW) {
+        if (K + 1 + p <= J1) {   // (the ring slot of a tile that does not exist may hold garbage)
+            const double* xs = ring + ((K + 1 + p) % (w + 1)) * TB + q * 16;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) acc += rn[c].x * xs[2 * c] + rn[c].y * xs[2 * c + 1];
+        }
+        for (int64_t J = K + 1 + p + NW; J <= J1; J += NW) {   // further tiles when NW < w
             const double2* Rt = reinterpret_cast<const double2*>(R + ((K * (w + 1)) + (J - K)) * TT + r * TB + q * 16);
             const double* xs = ring + (J % (w + 1)) * TB + q * 16;
 #pragma unroll
@@ -548,18 +567,21 @@ __global__ __launch_bounds__(BLOCK) void k_band_bsub(const double* __restrict__ 
         acc += __shfl_xor(acc, 2);
         double* pb = part + (K & 1) * NW * TB;
         if (q == 0) pb[p * TB + r] = acc;
+        double dk[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) dk[c] = dn[c];
+        fetch(K - 1);
         if (NW > 1 && !grid_barrier(bar, NW, gen)) return;
         const int64_t j = K * TB + r;
         if (q == 0) {
-            double s = 0.0;
-            for (unsigned int pp = 0; pp < NW; ++pp) s += pb[pp * TB + r];
-            Y[r] = (j < n ? v[j] * scale : 0.0) - s;
+            double sum = 0.0;
+            for (unsigned int pp = 0; pp < NW; ++pp) sum += pb[pp * TB + r];
+            Y[r] = (j < n ? v[j] * scale : 0.0) - sum;
         }
         __syncthreads();
-        const double* Dr = D + K * TT + r * TB + q * 16;   // x̃_K = D_K Y (D upper)
-        double x = 0.0;
+        double x = 0.0;   // x̃_K = D_K Y (D upper)
 #pragma unroll
-        for (int c = 0; c < 16; ++c) x += Dr[c] * Y[q * 16 + c];
+        for (int c = 0; c < 16; ++c) x += dk[c] * Y[q * 16 + c];
         x += __shfl_xor(x, 1);
         x += __shfl_xor(x, 2);
         if (q == 0) {
@@ -573,7 +595,8 @@ __global__ __launch_bounds__(BLOCK) void k_band_bsub(const double* __restrict__ 
 // vout = R̃⁻ᵀ (S Pᵀ t) with LSQR's epilogue (as dense.hip's k_gemvT_upper mode 1):
 // ỹ_K = D_Kᵀ (t̃_K − Σ_{I=K−w}^{K−1} R̃_IKᵀ ỹ_I), vout_j = ỹ_j/β − β vin_j/α (vin_j when β = 0),
 // part[0] = Σ vout².  Workgroup p takes the tiles K − 1 − I ≡ p (mod NW); thread (c = t%64,
-// q = t/64) rows q·16 .. q·16+15 of column c of each.
+// q = t/64) rows q·16 .. q·16+15 of column c of each; the next step's first tile and D column
+// segment are loaded before the barrier.
 __global__ __launch_bounds__(BLOCK) void k_band_fsub(const double* __restrict__ R, const double* __restrict__ D,
                                                      int64_t T, int w, int64_t n, const double* __restrict__ tin,
                                                      const LsqState* __restrict__ st, const double* __restrict__ vin,
@@ -588,15 +611,39 @@ __global__ __launch_bounds__(BLOCK) void k_band_fsub(const double* __restrict__ 
     const unsigned int NW = gridDim.x, p = blockIdx.x;
     unsigned int gen = 0;
     const int t = threadIdx.x, c = t & 63, q = t >> 6;
+    double rn[16], dn[16];
+    auto fetch = [&](int64_t K) {
+        const int64_t I = K - 1 - p;
+        const bool has = K < T && I >= max<int64_t>(0, K - w);
+        const double* Rt = R + ((I * (w + 1)) + (K - I)) * TT + (q * 16) * TB + c;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) rn[r] = has ? Rt[r * TB] : 0.0;
+        const double* Dc = D + (K < T ? K : 0) * TT + (q * 16) * TB + c;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dn[r] = K < T ? Dc[r * TB] : 0.0;
+    };
     double sv = 0.0;
+    fetch(0);
     for (int64_t K = 0; K < T; ++K) {
         double acc = 0.0;
-        for (int64_t I = K - 1 - p; I >= max<int64_t>(0, K - w); I -= NW) {
+        {
+            const int64_t I = K - 1 - p;
+            if (I >= max<int64_t>(0, K - w)) {
+                const double* ys = ring + (I % (w + 1)) * TB + q * 16;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc += rn[r] * ys[r];
+            }
+        }
+        for (int64_t I = K - 1 - p - NW; I >= max<int64_t>(0, K - w); I -= NW) {
             const double* Rt = R + ((I * (w + 1)) + (K - I)) * TT + (q * 16) * TB + c;
             const double* ys = ring + (I % (w + 1)) * TB + q * 16;
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc += Rt[r * TB] * ys[r];
         }
+        double dk[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dk[r] = dn[r];
+        fetch(K + 1);
         P4[q][c] = acc;
         __syncthreads();
         double* pb = part + (K & 1) * NW * TB;
@@ -604,15 +651,14 @@ __global__ __launch_bounds__(BLOCK) void k_band_fsub(const double* __restrict__ 
         if (NW > 1 && !grid_barrier(bar, NW, gen)) return;
         const int64_t j = K * TB + c;
         if (q == 0) {
-            double s = 0.0;
-            for (unsigned int pp = 0; pp < NW; ++pp) s += pb[pp * TB + c];
-            Z[c] = (j < n ? tin[perm[j]] * sc[j] : 0.0) - s;
+            double sum = 0.0;
+            for (unsigned int pp = 0; pp < NW; ++pp) sum += pb[pp * TB + c];
+            Z[c] = (j < n ? tin[perm[j]] * sc[j] : 0.0) - sum;
         }
         __syncthreads();
-        const double* Dc = D + K * TT + (q * 16) * TB + c;   // (D_Kᵀ Z)_c = Σ_r D[r][c] Z[r]
-        double y = 0.0;
+        double y = 0.0;   // (D_Kᵀ Z)_c = Σ_r D[r][c] Z[r]
 #pragma unroll
-        for (int r = 0; r < 16; ++r) y += Dc[r * TB] * Z[q * 16 + r];
+        for (int r = 0; r < 16; ++r) y += dk[r] * Z[q * 16 + r];
         P4[q][c] = y;
         __syncthreads();
         if (q == 0) {
@@ -806,8 +852,16 @@ void band_precond(System& S) {
     }
 }
 
-// workgroups of the multi-workgroup triangular solves (≤ 64: co-resident on any 256-CU device)
-int band_nw(const BandFactor& F) { return std::max(1, std::min(F.w, 64)); }
+// workgroups of the multi-workgroup triangular solves: co-resident on any device, and few — the
+// barrier's arrivals are atomics on one address, which serialise (LSQ_BAND_NW; at 1025²: 8
+// workgroups 0.75 s of triangular solves, 16: 0.78 s, 32 or 64: 1.05 s)
+int band_nw(const BandFactor& F) {
+    static const int cap = [] {
+        const char* e = getenv("LSQ_BAND_NW");
+        return e ? std::max(1, std::min(atoi(e), 64)) : 8;
+    }();
+    return std::max(1, std::min(F.w, cap));
+}
 
 void band_solve_scratch(System& S) {
     BandFactor& F = S.band;
