@@ -150,3 +150,17 @@ def test_smooth_fit_compute_E_band_equals_dense(gpu_available):
         assert np.array_equal(ok, np.isfinite(a)), k
         assert _rel(a[ok], b[ok]) < 1e-10, k
     assert out['band']['timing']['E_band']['tiles'] >= 1
+
+
+def test_band_empty_and_single_column_op_rows(gpu_available):
+    """op rows with no entries give 0; a row with one entry gives |v|·E of its column."""
+    S, fs, w = _small_system(10, 4)
+    n = fs.keep_cols.size
+    op = sp.csr_matrix((np.array([2.0, -3.0]), (np.array([1, 3]), np.array([0, n - 1]))), shape=(4, n))
+    try:
+        _prepare(fs, w, np.ones(fs.n_data, bool))
+        E, oe, info = fs.solver.cov_band(band_order(S['grids'], fs.keep_cols), op)
+    finally:
+        fs.close()
+    assert oe[0] == 0.0 and oe[2] == 0.0
+    assert abs(oe[1] - 2.0 * E[0]) <= 1e-12 * E[0] and abs(oe[3] - 3.0 * E[n - 1]) <= 1e-12 * E[n - 1]

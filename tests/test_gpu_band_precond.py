@@ -65,3 +65,35 @@ def test_sparseqr_compat_aniso_notebook(gpu_available, nodes, npts):
     xs = _exact(A, b)
     assert st['istop'] in (1, 2) and st['iters'] <= 40, st
     assert np.linalg.norm(x - xs) / np.linalg.norm(xs) < 1e-7
+
+
+def test_precond5_row_mask_reweight_and_tiny_systems(gpu_available):
+    """Row masks and re-weighting refactor the band (the factor follows the row scaling); a
+    single-tile system (T = 1, w = 0) and a 2-tile one take the same code path."""
+    for nodes in (5, 9, 61):
+        A, b, g = aniso.system(nodes, npts=50)
+        A = sp.csr_matrix(A)
+        rng = np.random.default_rng(nodes)
+        keep = rng.random(A.shape[0]) > 0.1
+        keep[8:] = True                                     # keep every constraint row
+        w = rng.uniform(0.5, 2.0, A.shape[0])
+        Ak = (sp.diags(w * keep) @ A).tocsr()
+        xs = _exact(Ak, w * keep * b)
+        with LSQSolver(0) as s:
+            Ac = A.tocoo()
+            s.set_matrix_coo(Ac.shape[0], Ac.shape[1], Ac.row, Ac.col, Ac.data)
+            x0, _ = s.solve(b, atol=1e-12, btol=1e-12, precond=5)          # factor for unit weights
+            s.set_row_weight(w)
+            s.set_row_mask(keep)
+            x, st = s.solve(b, atol=1e-12, btol=1e-12, precond=5)          # must refactor
+        assert st['istop'] in (1, 2) and st['iters'] <= 30, (nodes, st)
+        assert np.linalg.norm(x - xs) / np.linalg.norm(xs) < 1e-8, nodes
+
+
+def test_precond5_rank_deficient_raises(gpu_available):
+    from lssurf_amd._native import NativeError
+    A = sp.coo_matrix(np.array([[1.0, 1.0, 0.0], [2.0, 2.0, 0.0], [0.0, 0.0, 1.0]]))   # columns 0, 1 equal
+    with LSQSolver(0) as s:
+        s.set_matrix_coo(3, 3, A.row, A.col, A.data)
+        with pytest.raises(NativeError):
+            s.solve(np.ones(3), precond=5)
