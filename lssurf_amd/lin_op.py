@@ -18,6 +18,8 @@ generated which rows.  lssurf_amd's device path uses it to know an operator is a
 stencil/interp operator; methods that rescale values by data (normalize_by_unit_product,
 masks) drop the structure.
 """
+import weakref
+
 import numpy as np
 import scipy.sparse as sp
 
@@ -56,8 +58,30 @@ def _grad2_dzdt_parts(g, DOF, t):
                                       [-t, -t, -t, -t, 0, 0, 0, 0]), cxy)]
 
 
+_RANGES = {}   # id(array) -> (weakref, first, last): TOC arrays this module made with _arange
+
+
+def _arange(lo, hi, dtype=int):
+    """np.arange(lo, hi), remembered as a contiguous range (TOC rows / cols of 10⁷–10⁸ entries:
+    consumers then slice instead of scanning or fancy-indexing them)."""
+    a = np.arange(lo, hi, dtype=dtype)
+    if a.size:
+        key = id(a)
+        _RANGES[key] = (weakref.ref(a, lambda _r, k=key: _RANGES.pop(k, None)), int(lo), int(hi) - 1)
+    return a
+
+
+def known_range(a):
+    """(first, last) of an array made by _arange (and not since replaced), else None."""
+    e = _RANGES.get(id(a))
+    return (e[1], e[2]) if e is not None and e[0]() is a else None
+
+
 def _as_range(a):
     """(first, last) when `a` is a contiguous ascending integer range, else None."""
+    kr = known_range(a)
+    if kr is not None:
+        return kr
     a = np.asarray(a)
     if a.ndim != 1 or a.size == 0 or a.dtype.kind not in 'iu':
         return None
@@ -89,6 +113,8 @@ def _union_sorted(arrays):
         else:
             merged.append([lo, hi])
     dtype = np.result_type(*[np.asarray(a).dtype for a in arrays])
+    if len(merged) == 1:
+        return _arange(merged[0][0], merged[0][1] + 1, dtype=dtype)
     return np.concatenate([np.arange(lo, hi + 1, dtype=dtype) for lo, hi in merged])
 
 
@@ -97,7 +123,7 @@ def _grid_cols(g):
     key = (g.col_0, g.N_nodes)
     cached = getattr(g, '_toc_cols', None)
     if cached is None or cached[0] != key:
-        cached = (key, np.arange(g.col_0, g.col_0 + g.N_nodes))
+        cached = (key, _arange(g.col_0, g.col_0 + g.N_nodes))
         g._toc_cols = cached
     return cached[1]
 
@@ -227,7 +253,7 @@ class lin_op:
             n_eq = self._r.shape[0]
             self.parts = None
         self.N_eq = n_eq
-        self.TOC['rows'] = {self.name: np.arange(self.N_eq)}
+        self.TOC['rows'] = {self.name: _arange(0, self.N_eq)}
         self.TOC['cols'] = {g.name: _grid_cols(g)}
         self.__update_size_and_shape__()
         return self
@@ -374,11 +400,17 @@ class lin_op:
                 label = f'{base}_{k}'
             pieces = []
             for key, rows in op.TOC['rows'].items():
-                shifted = np.array(rows, dtype='int') + offset
+                kr = known_range(rows)
+                shifted = _arange(kr[0] + offset, kr[1] + 1 + offset) if kr is not None else \
+                    np.array(rows, dtype='int') + offset
                 self.TOC['rows'][key] = shifted
                 pieces.append(shifted.ravel())
             if label not in self.TOC['rows']:
-                self.TOC['rows'][label] = np.concatenate(pieces)
+                rr = [known_range(pc) for pc in pieces]
+                if all(r is not None for r in rr) and all(b[0] == a[1] + 1 for a, b in zip(rr, rr[1:])):
+                    self.TOC['rows'][label] = _arange(rr[0][0], rr[-1][1] + 1)   # consecutive ranges
+                else:
+                    self.TOC['rows'][label] = np.concatenate(pieces)
             if parts is not None and op.parts is not None:
                 parts.extend(dict(p, row0=p['row0'] + offset) for p in op.parts)
             else:
@@ -395,7 +427,7 @@ class lin_op:
         if ee:
             self.expected = np.concatenate(ee)
         if self.name is not None and len(self.name) > 0:
-            self.TOC['rows'][self.name] = np.arange(0, offset)
+            self.TOC['rows'][self.name] = _arange(0, offset)
         self.parts = parts
         self.__update_size_and_shape__()
         return self

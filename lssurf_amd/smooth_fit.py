@@ -27,7 +27,7 @@ from .constraint_functions import build_reference_epoch_matrix, node_column_bloc
     setup_smoothness_constraints
 from .grid_functions import setup_averaging_ops, setup_avg_mask_ops, setup_grids, setup_z0_avg, \
     validate_by_dz_mask
-from .lin_op import lin_op
+from .lin_op import known_range, lin_op
 from .assemble import describe
 from .solver import LSQSolver
 
@@ -168,7 +168,9 @@ def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grid
     x = None
     rs_data = None
     timing['lsq_iters'] = 0
-    weight0 = 1. / np.sqrt(E_all ** 2)     # TCinv diagonal, smooth_fit.py:129 (unchanged unless relaxed)
+    weight0 = np.square(E_all)             # TCinv diagonal 1/sqrt(E²), smooth_fit.py:129 (in place: 75 M rows)
+    np.sqrt(weight0, out=weight0)
+    np.divide(1., weight0, out=weight0)
     for iteration in range(args['max_iterations']):
         weight = weight0
         if last_iteration and args['sigma_extra_relax']:
@@ -256,6 +258,9 @@ def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grid
 
 def _as_slice(idx):
     """A contiguous ascending index array as a slice (no fancy-indexing copy of 73 M rows)."""
+    kr = known_range(idx)
+    if kr is not None:
+        return slice(kr[0], kr[1] + 1)
     idx = np.asarray(idx)
     if idx.ndim == 1 and idx.size and idx[-1] - idx[0] == idx.size - 1 and np.all(idx[1:] - idx[:-1] == 1):
         return slice(int(idx[0]), int(idx[-1]) + 1)
@@ -409,7 +414,8 @@ def smooth_fit(**kwargs):
         raise ValueError('zero value found in constraint sigma')
     if args['DEBUG']:
         print_TOC(G_data, Gc)
-    TCinv_diag = 1. / np.concatenate((Ed, Ec))
+    TCinv_diag = np.concatenate((Ed, Ec))
+    np.divide(1., TCinv_diag, out=TCinv_diag)
     rhs = np.zeros([N_eq])
     rhs[0:data.size] = data.z.ravel()
     for op in constraint_op_list:   # rhs[data.size:] = the concatenated priors
