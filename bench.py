@@ -209,8 +209,8 @@ def main():
     ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--config', default='c4')
     ap.add_argument('--no-solve', action='store_true', help='skip the full solve to tolerance')
-    ap.add_argument('--cpu-iters', type=int, default=60,
-                    help='LSQR iterations of the CPU baseline sample (~10 s on 16 host threads at C4)')
+    ap.add_argument('--cpu-iters', type=int, default=80,
+                    help='LSQR iterations of the CPU baseline sample (~11 s on 16 host threads at C4)')
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--dist', action='store_true', help='use the distributed (RCCL) path even at N=1')
     ap.add_argument('--no-pmc', action='store_true', help='skip the rocprofv3 PMC traffic passes')
