@@ -168,6 +168,7 @@ struct CgGrid {
     int32_t rowlen, coefc0;                  // coefficients per (cy, cx) class row; first of this grid
     int32_t gdy[CG_MAX_GRP];                 // dim-0 offset dy of group g
     int32_t gl[CG_MAX_GRP];                  // in-row LDS offset dx·tpad of group g
+    int32_t gdx[CG_MAX_GRP];                 // dim-1 offset dx of group g (multigrid tile kernel)
     int32_t gc[CG_MAX_GRP];                  // offset of group g's MAXT × (2·DT_g + 1) coefficients in a row
 };
 struct BlkAffine {
