@@ -843,6 +843,8 @@ void band_factor(System& S, const int32_t* h_perm, BandFactor& F) {
 constexpr int BAND_PRECOND_WMAX = 300;
 
 void band_precond(System& S) {
+    // a refactor reallocates R, D, sc and perm: captured LSQR batches hold the old pointers
+    graph_cache_drop(&S);
     band_factor(S, S.band_order.empty() ? nullptr : S.band_order.data(), S.band);
     if (S.band.w > BAND_PRECOND_WMAX) {
         S.band.valid = false;
@@ -850,6 +852,7 @@ void band_precond(System& S) {
                                     " tiles wide (at most " + std::to_string(BAND_PRECOND_WMAX) +
                                     "); set a bandwidth-reducing order (lsq_set_band_order)");
     }
+    band_solve_scratch(S);   // partial sums and barrier sized here, never inside a graph capture
 }
 
 // workgroups of the multi-workgroup triangular solves: co-resident on any device, and few — the

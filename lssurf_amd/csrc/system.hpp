@@ -369,6 +369,8 @@ void ensure_sell(System& S);                    // assembled A / AT (lazy when S
 void refresh_scaling(System& S, int precond);
 // band.hip: sqrt(diag((AᵀA)⁻¹)) and op-row variances from a banded Cholesky + Takahashi inverse
 void band_factor(System& S, const int32_t* perm, BandFactor& F);
+void graph_cache_drop(const System* S);   // lsqr.hip: captured iteration batches of S
+void band_solve_scratch(System& S);
 void band_precond(System& S);   // S.band from S.band_order (precond 5)
 void band_launch_bsub(System& S, const double* v, int scale_mode, double* out);
 void band_launch_fsub(System& S, const double* t, const double* vin, double* vout, double* part);
