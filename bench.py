@@ -57,7 +57,7 @@ def build_system(config, device):
     return fs, rhs, w, {'host_assembly_s': t1 - t0, 'device_formation_s': t2 - t1}
 
 
-def build_dist_system(config, rank, world, device, local_mg=False):
+def build_dist_system(config, rank, world, device):
     """One rank of the y-slab distributed system (lssurf_amd.dist): every rank assembles the
     (lazy) operator description, generates only its own rows on its GPU and joins the RCCL
     communicator."""
@@ -70,7 +70,7 @@ def build_dist_system(config, rank, world, device, local_mg=False):
     S = LS.smooth_fit(data=D, return_fit_objects=True, VERBOSE=False, **kw)
     keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch'])
     t1 = time.time()
-    ds = DistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, rank, world, device, local_mg=local_mg)
+    ds = DistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, rank, world, device)
     E_all = 1 / (1. / np.concatenate((S['Ed'], S['Ec'])))
     w = 1. / np.sqrt(E_all ** 2)
     rhs = np.zeros(w.size)
@@ -258,9 +258,7 @@ def main():
         os.environ.setdefault('NCCL_IB_DISABLE', '1')
         local = 0
     if world > 1 or args.dist:
-        # CGNR ranks also get their local multigrid systems for the solve (precond 4 over ranks)
-        ds, rhs, w, setup = build_dist_system(args.config, rank, world, local,
-                                              local_mg=meth == 1 and not args.no_solve and args.solve_precond in ('auto', '4'))
+        ds, rhs, w, setup = build_dist_system(args.config, rank, world, local)
         solver = _Dist(ds)
         fs = ds
     else:
@@ -314,15 +312,12 @@ def main():
     solve = {}
     if not args.no_solve:
         # solve wall-time with smooth_fit's default solver for this system: CGNR + the multigrid
-        # V-cycle (precond 4) where it runs (per-node blocks; over ranks one V-cycle per rank on
-        # its owned rows), else the timed configuration; then CGNR + block-Jacobi and (one GPU)
-        # LSQR + block-Jacobi for comparison
+        # V-cycle (precond 4) where it runs (single GPU, per-node blocks), else the timed
+        # configuration; then CGNR + block-Jacobi and LSQR + block-Jacobi for comparison
         names = {1: 'column scaling', 3: 'block-Jacobi per (y,x) node', 4: 'multigrid V-cycle (block-Jacobi smoothing)'}
-        if isinstance(solver, _Dist):
-            names[4] = 'multigrid V-cycle per rank (owned rows; block-Jacobi smoothing)'
         sp = args.precond
-        mg_ok = solver.ds.mgl is not None if isinstance(solver, _Dist) else solver.cg_available(4)[0]
-        if (args.solve_precond == 'auto' and meth == 1 and args.precond == 3 and mg_ok) or args.solve_precond == '4':
+        if (args.solve_precond == 'auto' and meth == 1 and not isinstance(solver, _Dist) and args.precond == 3
+                and solver.cg_available(4)[0]) or args.solve_precond == '4':
             sp = 4
 
         def rec(st):
@@ -331,9 +326,6 @@ def main():
         x, sst = solver.solve(rhs, op=args.op, precond=sp, method=meth)
         solve = dict(rec(sst), solve_method=['lsqr', 'cgnr'][int(sst.get('method', 0))],
                      solve_precond=names.get(sp, sp))
-        if meth == 1 and isinstance(solver, _Dist) and sp == 4:
-            _, sb = solver.solve(rhs, op=args.op, precond=3, method=1)
-            solve['solve_block_jacobi'] = rec(sb)
         if meth == 1 and not isinstance(solver, _Dist):   # distributed LSQR has no block-Jacobi
             if sp == 4:
                 xb, sb = solver.solve(rhs, op=args.op, precond=3, method=1)

@@ -231,17 +231,6 @@ int lsq_dist_set_halo(lsq_handle* h, int32_t n_ranges, const int64_t* own_ranges
                       const int32_t* peers, const int64_t* send_cnt, const int32_t* send_idx,
                       const int64_t* recv_cnt, const int32_t* recv_idx);
 
-/* CGNR + multigrid over ranks (lsq_opts.precond = 4, method = 1).  `local` is a separate
- * single-GPU handle on the same device holding the rank's OWNED node rows as a standalone
- * structured system (sub-grids of the owned rows; the stencil rows whose templates and the data
- * rows whose interpolation cells lie inside them; the global row weights of those rows via
- * lsq_set_row_weight on `local`; its node column blocks).  Its V-cycle is the rank's diagonal
- * block of the preconditioner.  seg = n_seg triples (window local full offset, `local` full
- * offset, length) mapping the owned columns.  `local` must outlive every precond-4 solve of h;
- * local = NULL unlinks.  Replaces no reference call: SuiteSparseQR (smooth_fit.py:142) is a
- * direct solver — this is the iterative replacement's preconditioner on rows of GPUs. */
-int lsq_dist_set_local_mg(lsq_handle* h, lsq_handle* local, int64_t n_seg, const int64_t* seg);
-
 /* Virtual ranks: the same distributed solve with every rank of the partition in THIS process
  * on one device (exchanges become device copies).  Configure each rank's handle exactly as a
  * real rank (lsq_set_col_map, lsq_set_matrix_*, lsq_dist_referenced_cols,

@@ -257,11 +257,9 @@ int lsq_solve(lsq_handle* h, const double* b, double* x_inout, const lsq_opts* o
         if (o->method != 0 && o->method != 1) return fail(S, "lsq_solve: method must be 0 (LSQR) or 1 (CGNR)");
         if (o->precond < 0 || o->precond > 5) return fail(S, "lsq_solve: precond must be 0 .. 5");
         if (o->precond == 5 && S.dist) return fail(S, "lsq_solve: precond 5 (band factor) is single-GPU");
-        if (o->precond == 4 && (o->method != 1 || (S.dist ? !S.mg_local : !lsq::cg_available(S, 4))))
-            return fail(S, "lsq_solve: precond 4 (multigrid) runs CGNR (method 1) on structured systems: " +
-                               (o->method != 1 ? std::string("method is not 1")
-                                : S.dist ? std::string("distributed rank without a local system (lsq_dist_set_local_mg)")
-                                : S.cg_ok ? S.mg_why : S.cg_why));
+        if (o->precond == 4 && (o->method != 1 || S.dist || !lsq::cg_available(S, 4)))
+            return fail(S, "lsq_solve: precond 4 (multigrid) runs CGNR (method 1) on single-GPU structured systems: " +
+                               (S.dist ? std::string("distributed rank") : o->method != 1 ? std::string("method is not 1") : S.cg_ok ? S.mg_why : S.cg_why));
         if (S.dist) {
             if (S.virt) return fail(S, "lsq_solve: a virtual rank solves through lsq_vgroup_solve");
             lsq::Group G;
@@ -291,11 +289,9 @@ int lsq_iterate(lsq_handle* h, const double* b, int64_t iters, const lsq_opts* o
         lsq_opts d;
         lsq_default_opts(&d);
         if (!o) o = &d;
-        if (o->precond == 4 && (o->method != 1 || (S.dist ? !S.mg_local : !lsq::cg_available(S, 4))))
-            return fail(S, "lsq_iterate: precond 4 (multigrid) runs CGNR (method 1) on structured systems: " +
-                               (o->method != 1 ? std::string("method is not 1")
-                                : S.dist ? std::string("distributed rank without a local system (lsq_dist_set_local_mg)")
-                                : S.cg_ok ? S.mg_why : S.cg_why));
+        if (o->precond == 4 && (o->method != 1 || S.dist || !lsq::cg_available(S, 4)))
+            return fail(S, "lsq_iterate: precond 4 (multigrid) runs CGNR (method 1) on single-GPU structured systems: " +
+                               (S.dist ? std::string("distributed rank") : o->method != 1 ? std::string("method is not 1") : S.cg_ok ? S.mg_why : S.cg_why));
         if (S.dist) {
             if (S.virt) return fail(S, "lsq_iterate: a virtual rank iterates through lsq_vgroup_iterate");
             lsq::Group G;
@@ -524,35 +520,6 @@ int lsq_dist_set_halo(lsq_handle* h, int32_t n_ranges, const int64_t* own_ranges
         S.dist_mf = true;
         S.cs_mode = -1;
         S.iter_ready = false;
-        return 0;
-    });
-}
-
-int lsq_dist_set_local_mg(lsq_handle* h, lsq_handle* local, int64_t n_seg, const int64_t* seg) {
-    return guarded(h, [&](lsq::System& S) {
-        if (!S.dist || !S.dist_mf) return fail(S, "lsq_dist_set_local_mg: not a structured rank (lsq_dist_set_halo first)");
-        lsq::graph_cache_drop(&S);
-        if (!local) {
-            S.mg_local = nullptr;
-            S.mgl_seg.clear();
-            return 0;
-        }
-        lsq::System& U = local->sys;
-        if (&U == &S || U.dist) return fail(S, "lsq_dist_set_local_mg: the local system must be a separate single-GPU handle");
-        if (U.device != S.device) return fail(S, "lsq_dist_set_local_mg: the local system lives on another device");
-        if (!U.G.rp.p) return fail(S, "lsq_dist_set_local_mg: the local system has no matrix");
-        if (n_seg < 1 || !seg) return fail(S, "lsq_dist_set_local_mg: no column segments");
-        for (int64_t k = 0; k < n_seg; ++k) {
-            const int64_t wo = seg[3 * k], lo = seg[3 * k + 1], len = seg[3 * k + 2];
-            if (wo < 0 || lo < 0 || len < 0 || wo + len > S.n_full || lo + len > U.n_full)
-                return fail(S, "lsq_dist_set_local_mg: a segment lies outside the window or the local system");
-        }
-        S.mgl_seg.assign(seg, seg + 3 * n_seg);
-        if (!S.ev_mgl0) {
-            HIP_CHECK(hipEventCreateWithFlags(&S.ev_mgl0, hipEventDisableTiming));
-            HIP_CHECK(hipEventCreateWithFlags(&S.ev_mgl1, hipEventDisableTiming));
-        }
-        S.mg_local = &U;
         return 0;
     });
 }

@@ -859,8 +859,6 @@ System::~System() {
     if (comm) (void)ncclCommDestroy(comm);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
-    if (ev_mgl0) (void)hipEventDestroy(ev_mgl0);
-    if (ev_mgl1) (void)hipEventDestroy(ev_mgl1);
     if (side) (void)hipStreamDestroy(side);
     if (stream && own_stream) (void)hipStreamDestroy(stream);
 }

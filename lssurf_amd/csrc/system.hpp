@@ -306,13 +306,6 @@ struct System {
     bool dist_mf = false;
     DBuf<int32_t> recv_idx;
     DBuf<uint8_t> live;
-    // CGNR + multigrid over ranks (precond 4, lsq_dist_set_local_mg): a standalone single-GPU
-    // system of the rank's owned node rows (the rows whose stencils and interpolation cells lie
-    // inside them); its V-cycle is the rank's diagonal block of the preconditioner.  mgl_seg:
-    // (window full offset, local full offset, length) triples of the owned columns.
-    System* mg_local = nullptr;
-    std::vector<int64_t> mgl_seg;
-    hipEvent_t ev_mgl0 = nullptr, ev_mgl1 = nullptr;
 
     // CGNR (method 1): normal-stencil description + coefficient table, rebuilt when the part
     // row scales change; vectors in the full column space

@@ -155,104 +155,6 @@ def window_problem(G_data, Gc, partition, rank, keep_cols):
                 keep_global=pos[keep_local], own_ranges=own_ranges, meta=meta, halo=halo)
 
 
-def local_problem(G_data, Gc, partition, rank, keep_cols):
-    """The rank's OWNED node rows as a standalone structured system — its diagonal block of the
-    multigrid preconditioner over ranks (lsq_dist_set_local_mg): sub-grids of the owned rows
-    [a, b), the stencil rows whose whole template lies inside them and the points whose
-    interpolation cell does (a margin of 1e-6 cells keeps the device's float subscripts inside).
-    Rows crossing a slab boundary are left out, so its AᵀA is an SPD approximation of the owned
-    block of the global AᵀA; the CG iteration carries the coupling."""
-    from ._native import GridDesc
-    (grid_descs, interp, (py, px, pt), stencils, npts), order = _describe_order(G_data, Gc)
-    meta, nloc = window_meta(order, partition, rank, 0)
-    grids = []
-    for gd, gm in zip(grid_descs, meta):
-        d = GridDesc.from_buffer_copy(gd)
-        d.shape[0] = gm['b'] - gm['a']
-        d.b0[0] = gd.b0[0] + gm['a'] * gd.delta[0]
-        d.col0 = gm['col0']
-        grids.append(d)
-    sel = partition.owner(py) == rank
-    for gi in set(int(i) for i in interp):
-        gd, gm = grid_descs[gi], meta[gi]
-        f = (py - gd.b0[0]) / gd.delta[0]
-        sel &= (f >= gm['a'] + 1e-6) & (f <= gm['b'] - 1 - 1e-6)
-    pts_in = np.flatnonzero(sel)
-    rows = [pts_in]
-    local = []
-    row0 = pts_in.size
-    for s, part in zip(stencils, Gc.parts):
-        gm = meta[s.grid]
-        oy = [int(s.off[t][0]) for t in range(s.ntpl)]
-        lo_y = max(int(s.lo[0]), gm['a'] - min(oy))
-        hi_y = min(int(s.hi[0]), gm['b'] - max(oy))
-        if lo_y >= hi_y:
-            continue
-        nd = int(order[s.grid].N_dims)
-        inner = int(np.prod([int(s.hi[d]) - int(s.lo[d]) for d in range(1, nd)]))
-        t = type(s).from_buffer_copy(s)
-        t.lo[0], t.hi[0] = lo_y - gm['a'], hi_y - gm['a']
-        t.n_eq = (hi_y - lo_y) * inner
-        t.row0 = row0
-        first = npts + int(part['row0']) + (lo_y - int(s.lo[0])) * inner
-        rows.append(first + np.arange(t.n_eq))
-        row0 += t.n_eq
-        local.append(t)
-    coords = (py[pts_in].copy(), px[pts_in].copy(), None if pt is None else pt[pts_in].copy())
-    l2g = np.concatenate([gm['gcol0'] + gm['a'] * gm['stride'] + np.arange((gm['b'] - gm['a']) * gm['stride'])
-                          for gm in meta])
-    keep_cols = np.asarray(keep_cols)
-    pos = np.minimum(np.searchsorted(keep_cols, l2g), keep_cols.size - 1)
-    keep_local = np.flatnonzero(keep_cols[pos] == l2g)
-    return dict(grids=grids, grid_objs=order, interp=interp, coords=coords, stencils=local, npts=int(pts_in.size),
-                rows=np.concatenate(rows), m=int(row0), n_full=int(nloc), keep=keep_local, l2g=l2g,
-                keep_global=pos[keep_local], own_ranges=[(gm['col0'], gm['col0'] + (gm['b'] - gm['a']) * gm['stride'])
-                                                         for gm in meta], meta=meta, halo=0)
-
-
-def local_segments(win, loc):
-    """(window full offset, local full offset, length) per grid: the owned columns of a rank's
-    window and of its local multigrid system (same grids, same node-row order)."""
-    seg = []
-    for gw, gl in zip(win['meta'], loc['meta']):
-        seg += [gw['col0'] + (gw['a'] - gw['wa']) * gw['stride'], gl['col0'], (gw['b'] - gw['a']) * gw['stride']]
-    return np.array(seg, np.int64)
-
-
-class _LocalMg:
-    """A rank's local multigrid system (single-GPU handle on the rank's device) linked to the
-    rank handle `h` for precond 4."""
-
-    def __init__(self, L, h, G_data, Gc, partition, rank, keep_cols, win, device):
-        self.L = L
-        self.prob = local_problem(G_data, Gc, partition, rank, keep_cols)
-        self.h = L.lsq_create(int(device))
-        if not self.h:
-            raise NativeError('lsq_create failed (local multigrid system)')
-        try:
-            _form_window(L, self.h, self.prob)
-            if not _install_blocks(L, self.h, self.prob, keep_cols):
-                raise NotImplementedError('multigrid over ranks needs node column blocks')
-            seg = local_segments(win, self.prob)
-            _HandleView(L, h).check(L.lsq_dist_set_local_mg(h, self.h, seg.size // 3, ptr(seg)),
-                                    'lsq_dist_set_local_mg')
-        except Exception:
-            L.lsq_destroy(self.h)
-            self.h = None
-            raise
-
-    def set_row_weight(self, w):
-        wl = as_c(np.asarray(w)[self.prob['rows']], np.float64)
-        _HandleView(self.L, self.h).check(self.L.lsq_set_row_weight(self.h, ptr(wl)), 'lsq_set_row_weight')
-
-    def close(self, h):
-        if self.h:
-            if h:
-                self.L.lsq_dist_set_local_mg(h, None, 0, None)
-            self.L.lsq_destroy(self.h)
-            self.h = None
-
-
 def window_halo(grid_objs, partition, rank, halo):
     """Halo lists of `rank` (local full ids, ascending global order): per peer, the owned
     columns the peer holds as ghosts (send) and the ghost columns the peer owns (recv)."""
@@ -461,8 +363,7 @@ class DistFitSystem(_Base):
     """One rank of a multi-GPU solve (RCCL).  `pg` is a torch.distributed process group used only
     for set-up (RCCL id broadcast, ghost lists); the solve itself never touches torch."""
 
-    def __init__(self, G_data, Gc, keep_cols, n_full, rank, nranks, device, pg=None, structured=True,
-                 local_mg=False):
+    def __init__(self, G_data, Gc, keep_cols, n_full, rank, nranks, device, pg=None, structured=True):
         if nranks > 1:
             import torch.distributed as tdist
         self.L = load()
@@ -486,8 +387,6 @@ class DistFitSystem(_Base):
                           window_halo(self.prob['grid_objs'], self.partition, rank, self.prob['halo']))
             self.has_blocks = _install_blocks(self.L, self.h, self.prob, keep_cols)
             self.n_x = self.prob['keep'].size
-            self.mgl = _LocalMg(self.L, self.h, G_data, Gc, self.partition, rank, keep_cols, self.prob, device) \
-                if local_mg else None   # precond 4: this rank's V-cycle system
         else:            # owned rows, relabelled compact columns, assembled SELL operator
             self.prob = rank_problem(G_data, Gc, self.partition, rank)
             flags = _form_rank(self.L, self.h, self.prob, keep_cols, n_full)
@@ -502,7 +401,6 @@ class DistFitSystem(_Base):
             self.owned_cols = self.layout[4]
             self.n_x = self.layout[2]
             self.has_blocks = False
-            self.mgl = None
         self.stats = None
 
     def scatter_owned(self, x_local, x_out):
@@ -523,12 +421,9 @@ class DistFitSystem(_Base):
     def set_row_weight(self, w):
         wl = as_c(np.asarray(w)[self.prob['rows']], np.float64)
         _HandleView(self.L, self.h).check(self.L.lsq_set_row_weight(self.h, ptr(wl)), 'lsq_set_row_weight')
-        if self.mgl is not None:
-            self.mgl.set_row_weight(w)
 
     def solve(self, row_weight, rhs, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, method=0):
-        """method 0: LSQR (precond 0/1); 1: CGNR (precond 1 Jacobi, 3 block-Jacobi, 4 multigrid with
-        local_mg=True; structured ranks)."""
+        """method 0: LSQR (precond 0/1); 1: CGNR (precond 1 Jacobi, 3 block-Jacobi; structured ranks)."""
         b = self._b(row_weight, rhs)
         x = np.zeros(self.n_x)
         o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond), method=int(method))
@@ -552,9 +447,6 @@ class DistFitSystem(_Base):
         return dict(zip(['m', 'n', 'nnz', 'sell_A', 'sell_AT', 'device_bytes', 'stencil_op', 'n_full'], o.tolist()))
 
     def close(self):
-        if getattr(self, 'mgl', None) is not None:
-            self.mgl.close(getattr(self, 'h', None))
-            self.mgl = None
         if getattr(self, 'h', None):
             self.L.lsq_destroy(self.h)
             self.h = None
@@ -564,7 +456,7 @@ class VirtualDistFitSystem(_Base):
     """All ranks of the partition in this process on one GPU (liblsqsurf virtual group):
     identical kernels, plans and exchange order as the RCCL path."""
 
-    def __init__(self, G_data, Gc, keep_cols, n_full, nranks, device=0, structured=True, local_mg=False):
+    def __init__(self, G_data, Gc, keep_cols, n_full, nranks, device=0, structured=True):
         self.L = load()
         self._setup_common(G_data, Gc, keep_cols, n_full, nranks)
         self.nranks = nranks
@@ -573,7 +465,6 @@ class VirtualDistFitSystem(_Base):
         if not self.g:
             raise NativeError('lsq_vgroup_create failed')
         self.probs = []
-        self.mgls = []
         if structured:
             for r in range(nranks):
                 h = self.L.lsq_vgroup_rank(self.g, r)
@@ -582,8 +473,6 @@ class VirtualDistFitSystem(_Base):
                 _install_halo(self.L, h, prob, window_halo(prob['grid_objs'], self.partition, r, prob['halo']))
                 _install_blocks(self.L, h, prob, keep_cols)
                 self.probs.append(prob)
-                if local_mg:
-                    self.mgls.append(_LocalMg(self.L, h, G_data, Gc, self.partition, r, keep_cols, prob, device))
             self.nx = [p['keep'].size for p in self.probs]
         else:
             flags_all = []
@@ -611,8 +500,6 @@ class VirtualDistFitSystem(_Base):
                 h = self.L.lsq_vgroup_rank(self.g, r)
                 wl = as_c(np.asarray(row_weight)[prob['rows']], np.float64)
                 _HandleView(self.L, h).check(self.L.lsq_set_row_weight(h, ptr(wl)), 'lsq_set_row_weight')
-            for m in self.mgls:
-                m.set_row_weight(row_weight)
         if rhs is not None:
             self._b_local = [as_c(np.asarray(rhs)[prob['rows']], np.float64) for prob in self.probs]
         return self._b_local
@@ -644,13 +531,10 @@ class VirtualDistFitSystem(_Base):
         return st.as_dict()
 
     def close(self):
-        for r, m in enumerate(getattr(self, 'mgls', [])):
-            m.close(self.L.lsq_vgroup_rank(self.g, r) if getattr(self, 'g', None) else None)
-        self.mgls = []
         if getattr(self, 'g', None):
             self.L.lsq_vgroup_destroy(self.g)
             self.g = None
 
 
-__all__ = ['SlabPartition', 'rank_problem', 'local_problem', 'local_segments', 'column_owner', 'local_layout', 'exchange_plan', 'DistFitSystem',
+__all__ = ['SlabPartition', 'rank_problem', 'column_owner', 'local_layout', 'exchange_plan', 'DistFitSystem',
            'VirtualDistFitSystem', 'LSQSolver']

@@ -181,34 +181,3 @@ def test_window_node_blocks_cover_window_in_global_order(nranks):
         assert np.unique(bcols).size == bcols.size            # a column in at most one block
     assert set(seen) == gblocks                               # every node block lives on some rank
     assert any(len(v) > 1 for v in seen.values())             # halo nodes are shared
-
-
-@pytest.mark.parametrize('nranks', [2, 3, 4])
-def test_local_multigrid_systems_stay_inside_owned_rows(nranks):
-    """dist.local_problem (the rank's block of the multigrid preconditioner over ranks): its rows
-    are rows of the global A that touch only the rank's owned columns, every stencil row of the
-    global A whose columns are all owned by the rank is there (the block loses only rows that
-    cross a slab boundary), and the column segments map its columns onto the window's owned
-    columns one to one."""
-    S, keep = _system()
-    A = _host_csr(S, keep)
-    part = dist.SlabPartition(S['grids']['dz'], nranks)
-    npts = S['G_data'].N_eq
-    seen_cols = []
-    for r in range(nranks):
-        win = dist.window_problem(S['G_data'], S['Gc'], part, r, keep)
-        loc = dist.local_problem(S['G_data'], S['Gc'], part, r, keep)
-        assert loc['m'] == loc['rows'].size == loc['npts'] + sum(s.n_eq for s in loc['stencils'])
-        owned = np.zeros(keep.size, bool)
-        owned[loc['keep_global']] = True
-        sub = A[loc['rows']]
-        assert np.all(owned[sub.indices]), r                          # rows stay inside the owned columns
-        cons = np.arange(npts, A.shape[0])
-        inside = np.array([owned[A.indices[A.indptr[i]:A.indptr[i + 1]]].all() and A.indptr[i + 1] > A.indptr[i]
-                           for i in cons])
-        np.testing.assert_array_equal(np.sort(loc['rows'][loc['npts']:]), cons[inside])
-        seg = dist.local_segments(win, loc).reshape(-1, 3)
-        for (wo, lo, n), gw, gl in zip(seg, win['meta'], loc['meta']):
-            np.testing.assert_array_equal(win['l2g'][wo:wo + n], loc['l2g'][lo:lo + n])
-        seen_cols.append(loc['keep_global'])
-    np.testing.assert_array_equal(np.sort(np.concatenate(seen_cols)), np.arange(keep.size))

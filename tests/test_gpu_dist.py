@@ -185,60 +185,3 @@ def test_virtual_ranks_cgnr_iterate_matches_solve_prefix(gpu_available):
     assert st['method'] == 1 and st['iters'] == 20 and st2['iters'] == 20
     assert np.isclose(st['r1norm'], st2['r1norm'], rtol=1e-10)
     assert np.all(np.isfinite(x))
-
-
-# ---- CGNR + multigrid over ranks (precond 4: a V-cycle per rank on its local system) ---------
-@pytest.mark.parametrize('nranks', [1, 2, 3, 4])
-def test_virtual_ranks_cgnr_multigrid(gpu_available, nranks):
-    """M⁻¹ = blockdiag of the ranks' V-cycles (each on the rank's owned rows, slab-crossing rows
-    left to CG): SPD, so PCG converges to the single-GPU solution; its iteration count stays a
-    small multiple of the single-GPU multigrid count and far below block-Jacobi's."""
-    S, kw = _t64()
-    keep, w, rhs = _problem(S, kw)
-    x1, st1 = _single_cg(S, keep, w, rhs, 4)
-    _, st3 = _single_cg(S, keep, w, rhs, 3)
-    vd = dist.VirtualDistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, nranks, local_mg=True)
-    try:
-        xd = vd.solve(w, rhs, atol=1e-12, btol=1e-12, conlim=1e12, precond=4, method=1)
-        std = vd.stats
-        # re-weighting reaches the local systems: a second solve with other weights
-        w2 = w * np.where(np.arange(w.size) < S['data'].size, 0.5, 1.0)
-        xd2 = vd.solve(w2, rhs, atol=1e-12, btol=1e-12, conlim=1e12, precond=4, method=1)
-    finally:
-        vd.close()
-    x2, _ = _single_cg(S, keep, w2, rhs, 4)
-    print(f'nranks {nranks}: multigrid over ranks {std["iters"]} iterations, single GPU multigrid {st1["iters"]}, '
-          f'block-Jacobi {st3["iters"]}')
-    assert std['method'] == 1 and std['istop'] in (1, 2), std
-    if nranks == 1:
-        assert abs(std['iters'] - st1['iters']) <= 3
-    assert std['iters'] <= max(3 * st1['iters'], 10) and std['iters'] < st3['iters'] // 2
-    assert np.linalg.norm(xd - x1) / np.linalg.norm(x1) <= 1e-8
-    assert np.linalg.norm(xd2 - x2) / np.linalg.norm(x2) <= 1e-8
-
-
-def test_virtual_ranks_cgnr_multigrid_golden_exact_solution(gpu_available):
-    g = golden('sys_sf3d.npz')
-    kw = golden_kwargs(g)
-    S = LS.smooth_fit(data=golden_points(g), return_fit_objects=True, **kw)
-    keep, w, rhs = _problem(S, kw)
-    vd = dist.VirtualDistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, 2, local_mg=True)
-    try:
-        x = vd.solve(w, rhs, atol=1e-12, btol=1e-12, conlim=1e12, maxit=200000, precond=4, method=1)
-    finally:
-        vd.close()
-    xs = g['x']
-    assert np.linalg.norm(x - xs) / np.linalg.norm(xs) <= 1e-6
-    assert np.max(np.abs(x - xs)) <= 1e-4
-
-
-def test_dist_multigrid_needs_local_system(gpu_available):
-    from lssurf_amd._native import NativeError
-    S, kw = _t64()
-    keep, w, rhs = _problem(S, kw)
-    vd = dist.VirtualDistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, 2)
-    try:
-        with pytest.raises(NativeError, match='local system'):
-            vd.solve(w, rhs, precond=4, method=1)
-    finally:
-        vd.close()
