@@ -194,7 +194,8 @@ struct MgHier;   // multigrid hierarchy (mg.inc)
 void mg_free(MgHier* h);
 struct CgDesc {
     int32_t n_grids, ntiles, lds_max, colmode;
-    int32_t nedge, maxt3, pad[2];            // column mode: workgroups of k_cg_xedge<1> (pad[0]: <8>); 3-D column length
+    int32_t nedge, maxt3, pad[2];            // column mode: workgroups of the CG iteration's k_cg_xedge (pad[0]: <8>;
+                                             // pad[1]: lanes per item of the CG iteration's pass, 1 or 8); 3-D column length
     CgGrid g[MF_MAX_GRIDS];
 };
 // CGNR data rows without a stored matrix (lsqr_cg.inc, k_cg_dmf_*): when every interpolation

@@ -23,12 +23,17 @@ CONFIGS = {
     't256': (256, 12, 131_072),
     'tdense': (64, 12, 40_000),   # ~10 points per cell: strips whose point runs overflow LDS staging
     't15': (80, 15, 12_000),        # 15 epochs: the 16-long register columns; 80 nodes: two strips per row
+    # one rank's window of C4 over 4 / 8 GPUs (owned node rows + 2 halo rows, 1/N of the points):
+    # the per-rank compute floor of the strong-scaling runs, measurable on one GPU
+    'c4y4': (1024, 12, 500_000, 258),
+    'c4y8': (1024, 12, 250_000, 130),
 }
 
 
 def config_kwargs(name, stiff=False):
-    n, nt, npts = CONFIGS[name]
-    W = {'x': (n - 1) * 100., 'y': (n - 1) * 100., 't': (nt - 1) * 0.25}
+    n, nt, npts = CONFIGS[name][:3]
+    ny = CONFIGS[name][3] if len(CONFIGS[name]) > 3 else n   # node rows (y) when not square
+    W = {'x': (n - 1) * 100., 'y': (ny - 1) * 100., 't': (nt - 1) * 0.25}
     return dict(W=W, ctr={'x': 0., 'y': 0., 't': 0.}, spacing={'z0': 100., 'dz': 100., 'dt': 0.25},
                 E_RMS=dict(E_RMS_STIFF if stiff else E_RMS_NOTEBOOK), reference_epoch=nt // 2), npts
 
