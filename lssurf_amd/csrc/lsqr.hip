@@ -361,6 +361,25 @@ __global__ __launch_bounds__(BLOCK) void k_pack(int64_t cnt, const int32_t* __re
         dst[k] = src[idx[k]];
 }
 
+// k_pack + k_red_parts in one launch (distributed CG): block 0 first reduces the step's scalar
+// partials into gs (k_red_parts' summation order), then every block packs
+__global__ __launch_bounds__(BLOCK) void k_pack_red(int64_t cnt, const int32_t* __restrict__ idx,
+                                                    const double* __restrict__ src, double* __restrict__ dst,
+                                                    const double* part_a, int na, int slot_a, const double* part_b,
+                                                    int nb, int slot_b, double* gs) {
+    if (blockIdx.x == 0) {
+        const double a = reduce_parts(part_a, na);
+        double b = 0.0;
+        if (part_b) b = reduce_parts(part_b, nb);
+        if (threadIdx.x == 0) {
+            gs[slot_a] = a;
+            if (part_b) gs[slot_b] = b;
+        }
+    }
+    for (int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x; k < cnt; k += (int64_t)gridDim.x * BLOCK)
+        dst[k] = src[idx[k]];
+}
+
 __global__ __launch_bounds__(BLOCK) void k_scatter_add(int64_t cnt, const int32_t* __restrict__ idx,
                                                        const double* __restrict__ src, double* __restrict__ dst) {
     for (int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x; k < cnt; k += (int64_t)gridDim.x * BLOCK)
