@@ -8,12 +8,12 @@ run() {   # name, env..., -- bench args
     local name=$1; shift
     timeout -k 10 300 env "$@" > $OUT/$name.json 2> $OUT/$name.err
 }
-run c4y8_auto LSQ_CG_XE=0 python3 bench.py --config c4y8 --dist --no-cpu --no-pmc --no-solve --steps 400 --warmup 20
+run c4y8_xe8 LSQ_CG_XE=8 python3 bench.py --config c4y8 --dist --no-cpu --no-pmc --no-solve --steps 400 --warmup 20
 run c4y8_xe1 LSQ_CG_XE=1 python3 bench.py --config c4y8 --dist --no-cpu --no-pmc --no-solve --steps 400 --warmup 20
 for ys in 4 12 16; do
   run c4y8_ys$ys LSQ_CG_YS=$ys python3 bench.py --config c4y8 --dist --no-cpu --no-pmc --no-solve --steps 400 --warmup 20
 done
-run c4y4_auto LSQ_CG_XE=0 python3 bench.py --config c4y4 --dist --no-cpu --no-pmc --no-solve --steps 400 --warmup 20
+run c4y4_xe8 LSQ_CG_XE=8 python3 bench.py --config c4y4 --dist --no-cpu --no-pmc --no-solve --steps 400 --warmup 20
 run c4y4_xe1 LSQ_CG_XE=1 python3 bench.py --config c4y4 --dist --no-cpu --no-pmc --no-solve --steps 400 --warmup 20
-run c4_auto LSQ_CG_XE=0 python3 bench.py --config c4 --no-cpu --no-pmc --steps 200 --warmup 20
+run c4_xe8 LSQ_CG_XE=8 python3 bench.py --config c4 --no-cpu --no-pmc --steps 200 --warmup 20
 echo ok > $OUT/ok
