@@ -181,3 +181,20 @@ def test_window_node_blocks_cover_window_in_global_order(nranks):
         assert np.unique(bcols).size == bcols.size            # a column in at most one block
     assert set(seen) == gblocks                               # every node block lives on some rank
     assert any(len(v) > 1 for v in seen.values())             # halo nodes are shared
+
+
+@pytest.mark.parametrize('name,nranks', [('c4y4', 4), ('c4y8', 8)])
+def test_slab_configs_are_one_rank_window_of_c4(name, nranks):
+    """synthetic 'c4y4' / 'c4y8' (the per-rank compute floor of bench --gpus 4 / 8):
+    the node-row count of one interior rank's window of C4 (owned rows + halo rows), C4's row
+    width, epochs and spacing, and 1/N of C4's points."""
+    from lssurf_amd import synthetic
+    n, nt, npts = synthetic.CONFIGS['c4']
+    kw, pts = synthetic.config_kwargs(name)
+    ck, cpts = synthetic.config_kwargs('c4')
+    assert pts * nranks == cpts and kw['spacing'] == ck['spacing'] and kw['W']['x'] == ck['W']['x']
+    ny = int(round(kw['W']['y'] / kw['spacing']['dz'])) + 1
+    halo = 1   # one ghost node row per side (the stencils and the interpolation reach one row)
+    assert ny == n // nranks + 2 * halo
+    D, _ = synthetic.points(name)
+    assert D.size == pts and np.all(np.abs(D.y) <= kw['W']['y'] / 2) and np.all(np.abs(D.x) <= kw['W']['x'] / 2)
