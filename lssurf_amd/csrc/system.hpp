@@ -196,6 +196,7 @@ struct CgDesc {
     int32_t n_grids, ntiles, lds_max, colmode;
     int32_t nedge, maxt3, pad[2];            // column mode: workgroups of the CG iteration's k_cg_xedge (pad[0]: <8>;
                                              // pad[1]: lanes per item of the CG iteration's pass, 1 or 8); 3-D column length
+    int32_t w8, pad2;                        // column mode: the CG iteration runs k_cg_normal_col8 (8-wave workgroups)
     CgGrid g[MF_MAX_GRIDS];
 };
 // CGNR data rows without a stored matrix (lsqr_cg.inc, k_cg_dmf_*): when every interpolation
