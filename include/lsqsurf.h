@@ -128,6 +128,17 @@ int lsq_set_matrix_stencil(lsq_handle* h, int64_t m, int64_t n_full,
                            int32_t n_stencil, const lsq_stencil_desc* stencils,
                            const double* row_weight);
 
+/* Field-valued (variable-coefficient) stencil part, staged before lsq_set_matrix_stencil: stencil
+ * index `stencil` of that call keeps its grid, rows and centre box, and its template becomes the
+ * ntpl (≤ 16) offsets off[3·t + d] with entry value val[t] · F[fsel[t]·n_eq + k] in the row of
+ * centre k (k = ravel of centre − lo over the box, the row order of lin_op.diff_op).  F holds the
+ * nfield exact per-row values (field-major).  This is the directional smoothing operator of
+ * notebooks/smooth_fit_demo_aniso.ipynb cells 9-10: a lin_op.diff_op template whose rows
+ * scale_op_by_2d_grid multiplies by the interpolated direction field (u², 2uv, v²), summed over
+ * three templates on the same rows — one part here, 9 entries, F = the distinct |values|. */
+int lsq_set_stencil_fields(lsq_handle* h, int32_t stencil, int32_t ntpl, const int32_t* off, const double* val,
+                           int32_t nfield, const int32_t* fsel, int64_t n_eq, const double* F);
+
 /* Replace the row weights (TCinv of iterate_fit, smooth_fit.py:123-129) without re-forming. */
 int lsq_set_row_weight(lsq_handle* h, const double* row_weight);
 /* Row selection Ip_r (smooth_fit.py:132-135): rows with keep[i] == 0 are excluded from the

@@ -43,7 +43,8 @@ class LsqStats(ctypes.Structure):
 
 # every symbol declared in include/lsqsurf.h
 EXPORTS = ['lsq_default_opts', 'lsq_create', 'lsq_destroy', 'lsq_last_error', 'lsq_set_col_map',
-           'lsq_set_matrix_coo', 'lsq_set_matrix_stencil', 'lsq_set_row_weight', 'lsq_set_row_mask',
+           'lsq_set_matrix_coo', 'lsq_set_matrix_stencil', 'lsq_set_stencil_fields', 'lsq_set_row_weight',
+           'lsq_set_row_mask',
            'lsq_set_column_blocks', 'lsq_shape', 'lsq_get_csr',
            'lsq_solve', 'lsq_spmv', 'lsq_spmv_rows', 'lsq_rows_sumsq', 'lsq_data_colsum', 'lsq_iterate', 'lsq_profile_kernels', 'lsq_cg_available', 'lsq_profile_cg', 'lsq_mg_info', 'lsq_mg_apply', 'lsq_normal_apply', 'lsq_sell_info', 'lsq_sigma_x', 'lsq_cov_band', 'lsq_set_band_order',
            'lsq_get_rinv', 'lsq_dist_unique_id', 'lsq_create_dist', 'lsq_dist_referenced_cols',
@@ -73,6 +74,7 @@ def load():
         'lsq_set_matrix_coo': ([P, i64, i64, i64, P, P, P, P], ctypes.c_int),
         'lsq_set_row_weight': ([P, P], ctypes.c_int),
         'lsq_set_matrix_stencil': ([P, i64, i64, i32, P, i32, P, i64, P, P, P, i32, P, P], ctypes.c_int),
+        'lsq_set_stencil_fields': ([P, i32, i32, P, P, i32, P, i64, P], ctypes.c_int),
         'lsq_set_row_mask': ([P, P], ctypes.c_int),
         'lsq_set_column_blocks': ([P, i64, P, P], ctypes.c_int),
         'lsq_shape': ([P, P, P, P], ctypes.c_int),

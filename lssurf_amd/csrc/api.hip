@@ -159,6 +159,35 @@ int lsq_set_matrix_stencil(lsq_handle* h, int64_t m, int64_t n_full, int32_t n_g
     });
 }
 
+int lsq_set_stencil_fields(lsq_handle* h, int32_t stencil, int32_t ntpl, const int32_t* off, const double* val,
+                           int32_t nfield, const int32_t* fsel, int64_t n_eq, const double* F) {
+    return guarded(h, [&](lsq::System& S) {
+        if (S.G.rp.p) return fail(S, "lsq_set_stencil_fields must precede lsq_set_matrix_stencil");
+        if (stencil < 0 || ntpl < 1 || ntpl > lsq::MF_MAXT || !off || !val || nfield < 1 || nfield > ntpl || !fsel ||
+            n_eq < 0 || (n_eq && !F))
+            return fail(S, "lsq_set_stencil_fields: bad arguments");
+        for (int t = 0; t < ntpl; ++t)
+            if (fsel[t] < 0 || fsel[t] >= nfield) return fail(S, "lsq_set_stencil_fields: fsel out of range");
+        S.sfields.erase(std::remove_if(S.sfields.begin(), S.sfields.end(),
+                                       [&](const lsq::System::StencilFields& f) { return f.stencil == stencil; }),
+                        S.sfields.end());
+        lsq::System::StencilFields f;
+        f.stencil = stencil;
+        f.ntpl = ntpl;
+        f.nfield = nfield;
+        for (int t = 0; t < ntpl; ++t) {
+            for (int d = 0; d < 3; ++d) f.off[t][d] = off[3 * t + d];
+            f.val[t] = val[t];
+            f.fsel[t] = fsel[t];
+        }
+        f.F.alloc(std::max<int64_t>((int64_t)nfield * n_eq, 1));
+        f.F.upload(F, (int64_t)nfield * n_eq, S.stream);
+        HIP_CHECK(hipStreamSynchronize(S.stream));
+        S.sfields.push_back(std::move(f));
+        return 0;
+    });
+}
+
 int lsq_set_row_weight(lsq_handle* h, const double* row_weight) {
     return guarded(h, [&](lsq::System& S) {
         if (!S.G.rp.p) return fail(S, "lsq_set_row_weight: no matrix");

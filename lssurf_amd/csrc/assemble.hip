@@ -24,13 +24,25 @@ namespace {
 
 constexpr int MAX_GRIDS = 4, MAX_INTERP = 4, MAX_STENCIL = 32, MAXE = 32;
 
+// one stencil part as the formation sees it: lsq_stencil_desc, or its field-valued override
+// (lsq_set_stencil_fields: ≤ MF_MAXT entries, value val[t] · F[fsel[t]·n_eq + k] for centre k)
+struct GenSt {
+    int32_t grid, ntpl;
+    int32_t off[MF_MAXT][3];
+    double val[MF_MAXT];
+    int32_t fsel[MF_MAXT];
+    int64_t row0, n_eq;
+    int64_t lo[3], hi[3];
+    const double* F;   // null: constant values
+};
+
 struct GenCtx {
     int32_t n_grids, n_interp, n_stencil, pad;
     int64_t npts, m, n_full;
     lsq_grid_desc grids[MAX_GRIDS];
     int64_t stride[MAX_GRIDS][3];
     int32_t interp_grid[MAX_INTERP];
-    lsq_stencil_desc st[MAX_STENCIL];
+    GenSt st[MAX_STENCIL];
 };
 
 __global__ __launch_bounds__(BLOCK) void k_gen_rows(int pass, const GenCtx* __restrict__ ctx,
@@ -76,10 +88,11 @@ __global__ __launch_bounds__(BLOCK) void k_gen_rows(int pass, const GenCtx* __re
         } else {
             int s = 0;
             while (s + 1 < ctx->n_stencil && r >= ctx->st[s + 1].row0) ++s;
-            const lsq_stencil_desc& S = ctx->st[s];
+            const GenSt& S = ctx->st[s];
             const lsq_grid_desc& g = ctx->grids[S.grid];
             const int nd = g.ndim;
-            int64_t rem = r - S.row0;
+            const int64_t k = r - S.row0;
+            int64_t rem = k;
             int64_t sub[3] = {0, 0, 0};
             for (int d = nd - 1; d >= 0; --d) {
                 const int64_t ext = S.hi[d] - S.lo[d];
@@ -90,7 +103,7 @@ __global__ __launch_bounds__(BLOCK) void k_gen_rows(int pass, const GenCtx* __re
                 int64_t col = g.col0;
                 for (int d = 0; d < nd; ++d) col += (sub[d] + S.off[t][d]) * ctx->stride[S.grid][d];
                 cols[ne] = col;
-                vals[ne] = S.val[t];
+                vals[ne] = S.F ? S.val[t] * S.F[S.fsel[t] * S.n_eq + k] : S.val[t];
                 ++ne;
             }
         }
@@ -149,7 +162,7 @@ __global__ __launch_bounds__(BLOCK) void k_gen_rows(int pass, const GenCtx* __re
 // every template entry of every centre in the box stays inside its grid, grids do not overlap,
 // and every index fits 31 bits.
 bool describe_stencil_operator(MfDesc& d, int64_t m, int64_t n_full, int32_t n_grids, const lsq_grid_desc* grids,
-                               int64_t npts, int32_t n_stencil, const lsq_stencil_desc* st) {
+                               int64_t npts, int32_t n_stencil, const GenSt* st) {
     d = MfDesc{};
     d.npts = npts;
     d.m = m;
@@ -172,7 +185,7 @@ bool describe_stencil_operator(MfDesc& d, int64_t m, int64_t n_full, int32_t n_g
     }
     d.n_grids = n_grids;
     for (int i = 0; i < n_stencil; ++i) {
-        const lsq_stencil_desc& S = st[i];
+        const GenSt& S = st[i];
         if (S.n_eq == 0) continue;
         if (d.n_parts == MF_MAX_PARTS) return false;
         MfGrid& G = d.g[S.grid];
@@ -209,21 +222,25 @@ bool describe_stencil_operator(MfDesc& d, int64_t m, int64_t n_full, int32_t n_g
                 P.ihi[k] = std::min<int32_t>(P.ihi[k], P.hi[k] + (int32_t)o);
             }
             P.val[t] = S.val[t];
+            P.fsel[t] = S.F ? S.fsel[t] : 0;
         }
+        P.var = S.F ? 1 : 0;
+        P.F = S.F;
+        P.nfield = 0;
+        for (int t = 0; t < S.ntpl; ++t) P.nfield = std::max(P.nfield, P.fsel[t] + 1);
         // Aᵀu validity of template t for a column c: lo <= c - off_t < hi in every dim, i.e.
         // off_t <= c - lo and off_t >= c - hi + 1.  With |off| <= MF_R both sides depend only on
         // a = clamp(c - lo + MF_R + 1, 0, 2 MF_R + 1) and b = clamp(c - hi + MF_R + 1, ...):
-        // byte a of mlo / byte b of mhi hold the templates valid on that side.
+        // mlo[k][a] / mhi[k][b] hold the templates valid on that side (bit t).
         for (int k = 0; k < 3; ++k) {
-            P.mlo[k] = P.mhi[k] = 0;
             for (int a = 0; a <= 2 * MF_R + 1; ++a) {
-                uint64_t lo_bits = 0, hi_bits = 0;
+                uint32_t lo_bits = 0, hi_bits = 0;
                 for (int t = 0; t < S.ntpl; ++t) {
-                    if (P.off[t][k] <= a - MF_R - 1) lo_bits |= uint64_t(1) << t;
-                    if (P.off[t][k] >= a - MF_R) hi_bits |= uint64_t(1) << t;
+                    if (P.off[t][k] <= a - MF_R - 1) lo_bits |= 1u << t;
+                    if (P.off[t][k] >= a - MF_R) hi_bits |= 1u << t;
                 }
-                P.mlo[k] |= lo_bits << (8 * a);
-                P.mhi[k] |= hi_bits << (8 * a);
+                P.mlo[k][a] = lo_bits;
+                P.mhi[k][a] = hi_bits;
             }
         }
         G.part[G.nparts++] = d.n_parts++;
@@ -313,9 +330,37 @@ void form_from_stencils(System& S, int64_t m, int64_t n_full, int32_t n_grids, c
     }
     if (ncorners > MAXE) throw std::invalid_argument("too many interpolation corners per row");
     int64_t expect = npts;
+    S.has_var = false;
     for (int s = 0; s < n_stencil; ++s) {
-        h.st[s] = st[s];
-        if (st[s].grid < 0 || st[s].grid >= n_grids || st[s].ntpl < 1 || st[s].ntpl > 8)
+        GenSt& G = h.st[s];
+        G.grid = st[s].grid;
+        G.ntpl = st[s].ntpl;
+        G.row0 = st[s].row0;
+        G.n_eq = st[s].n_eq;
+        for (int d = 0; d < 3; ++d) {
+            G.lo[d] = st[s].lo[d];
+            G.hi[d] = st[s].hi[d];
+        }
+        G.F = nullptr;
+        if (G.ntpl >= 1 && G.ntpl <= 8)
+            for (int t = 0; t < G.ntpl; ++t) {
+                for (int d = 0; d < 3; ++d) G.off[t][d] = st[s].off[t][d];
+                G.val[t] = st[s].val[t];
+                G.fsel[t] = 0;
+            }
+        for (const auto& f : S.sfields) {   // field-valued override (lsq_set_stencil_fields)
+            if (f.stencil != s) continue;
+            if (f.F.n < (int64_t)f.nfield * G.n_eq) throw std::invalid_argument("stencil fields: F too short");
+            G.ntpl = f.ntpl;
+            for (int t = 0; t < f.ntpl; ++t) {
+                for (int d = 0; d < 3; ++d) G.off[t][d] = f.off[t][d];
+                G.val[t] = f.val[t];
+                G.fsel[t] = f.fsel[t];
+            }
+            G.F = G.n_eq ? f.F.p : nullptr;
+            S.has_var = S.has_var || G.F;
+        }
+        if (G.grid < 0 || G.grid >= n_grids || G.ntpl < 1 || G.ntpl > (G.F ? MF_MAXT : 8))
             throw std::invalid_argument("bad stencil descriptor");
         if (st[s].row0 != expect) throw std::invalid_argument("stencil parts must tile rows [npts, m) in order");
         int64_t ext = 1;
@@ -361,7 +406,10 @@ void form_from_stencils(System& S, int64_t m, int64_t n_full, int32_t n_grids, c
     if (herr) throw std::invalid_argument("lsq_set_matrix_stencil: " + std::to_string(herr) +
                                           " nonzero entries fall outside [0, n_full)");
     S.n_sorted_rows = npts;   // data rows: point order is random in space
-    S.mf = !S.dist && describe_stencil_operator(S.mfh, m, n_full, n_grids, grids, npts, n_stencil, st);
+    S.mf = !S.dist && describe_stencil_operator(S.mfh, m, n_full, n_grids, grids, npts, n_stencil, h.st);
+    if (S.has_var && !S.mf)
+        throw std::invalid_argument("lsq_set_matrix_stencil: field-valued parts need the structured operator "
+                                    "(single GPU, parts inside their grids, |offsets| <= 3)");
     finish_formation(S);
     if (S.mf) build_dmf(S, n_grids, grids, n_interp, interp_grid, npts, py, px, pt);
 }

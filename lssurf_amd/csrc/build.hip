@@ -745,7 +745,7 @@ void scaling_fill_values(System& S, int precond, bool set_csf) {
         KERNEL_CHECK();
     }
     if (S.mf) {   // data rows carry the row scale only; the stencil kernels apply cs themselves
-        const int64_t npts = S.mfh.npts, nf = S.n_full;
+        const int64_t npts = S.mfh.npts;
         hipLaunchKernelGGL(k_sell_vals, dim3(grid_for(npts)), dim3(BLOCK), 0, st, npts, S.G.rp.p, S.G.ci.p,
                            S.G.val.p, S.rs.p, nullptr, 0, S.Ad.perm.p, S.Ad.sp.p, S.Ad.val.p);
         KERNEL_CHECK();

@@ -717,8 +717,9 @@ void run_batch(System& S, int count, bool use_graph, int precond, bool mf) {
 // Algorithmic HBM bytes per launch of the two streaming kernels (DESIGN.md §Byte model).
 // Assembled SELL: x/w+A·v = 12Z + 16m + 48n, Aᵀu = 12Z + 8m + 16n (Z = nnz, 12 B per entry).
 // Stencil operator (n_f full columns, Z_d entries of the m_d data rows, stencil part p with
-// n_p rows): x/w+A·v = 48 n_f + 12 Z_d + 16 m_d + Σ_p n_p (16 + 8 [row scale not constant]);
-// Aᵀu = 36 n_f + 12 Z_d + 8 m_d + Σ_p n_p (8 + 8 [...]).  Per column: y, w read+write, ṽ, zv
+// n_p rows): x/w+A·v = 48 n_f + 12 Z_d + 16 m_d + Σ_p n_p (16 + 8 [row scale not constant] +
+// 8 nfield [field-valued]); Aᵀu = 36 n_f + 12 Z_d + 8 m_d + Σ_p n_p (8 + 8 [...] + 8 nfield [...]).
+// Per column: y, w read+write, ṽ, zv
 // gathered once / cs, ṽ in, ṽ out, zv out, the 4-B ATd row offset.
 void kernel_bytes(const System& S, bool mf, double out[2]) {
     if (mf) {
@@ -726,8 +727,9 @@ void kernel_bytes(const System& S, bool mf, double out[2]) {
         double f = 48.0 * nf + 12.0 * zd + 16.0 * md, t = 36.0 * nf + 12.0 * zd + 8.0 * md;
         for (int p = 0; p < S.mfh.n_parts; ++p) {
             const double n = (double)S.mfh.p[p].n_eq, w = S.mfh.p[p].wconst ? 0.0 : 8.0;
-            f += n * (16.0 + w);
-            t += n * (8.0 + w);
+            const double fv = S.mfh.p[p].var ? 8.0 * S.mfh.p[p].nfield : 0.0;   // per-row field values
+            f += n * (16.0 + w + fv);
+            t += n * (8.0 + w + fv);
         }
         out[0] = f;
         out[1] = t;

@@ -55,6 +55,8 @@ struct Sell {
 // map (Ip_c) carry column scale 0, so they never enter the iteration (x_j stays 0), which is the
 // same LSQR as on the compacted matrix.
 constexpr int MF_MAX_PARTS = 32, MF_MAX_GRID_PARTS = 16, MF_MAX_GRIDS = 4;
+constexpr int MF_MAXT = 16;                  // template entries per part (constant parts: ≤ 8 from
+                                             // lsq_stencil_desc; field-valued parts: ≤ 16)
 constexpr int MF_NPT = 2;                    // nodes per thread per block iteration
 constexpr int MF_ALIGN = 256 * MF_NPT;       // node-enumeration alignment of every grid
 constexpr int MF_R = 3;                      // |template offset| <= MF_R (8 edge classes per side)
@@ -72,18 +74,25 @@ inline FastDiv make_fastdiv(uint32_t d) {
     f.mul = (uint64_t)(((unsigned __int128)1 << (32 + s)) + d - 1) / d;   // ceil(2^(32+s) / d)
     return f;
 }
+// Field-valued (variable-coefficient) parts — lsq_set_stencil_fields, e.g. the anisotropic
+// notebook's directional operator whose rows are scaled by a direction field: entry t of the row
+// of centre k (k = ravel_box(c − lo)) is val[t] · F[fsel[t]·n_eq + k] (val = ±1 there), with F
+// the nfield exact per-row values on the device.
 struct MfPart {
     int32_t grid, ntpl, row0, n_eq;          // rows [row0, row0 + n_eq) (global row ids < 2^31)
     int32_t lo[3], hi[3], bstride[3];
     int32_t ilo[3], ihi[3];                  // centres whose every template entry hits the box
-    int32_t off[8][3];
-    int32_t doff[8];                         // column offset of template entry t  (Σ off·stride)
-    int32_t boff[8];                         // row offset of template entry t     (Σ off·bstride)
-    uint64_t mlo[3], mhi[3];                 // template validity masks by edge class (MF_R)
-    int32_t loff[8];                         // A·v: LDS offset of template t (MfGrid bands)
-    int32_t wconst, pad;                     // 1: every row of the part has row scale w
+    int32_t off[MF_MAXT][3];
+    int32_t doff[MF_MAXT];                   // column offset of template entry t  (Σ off·stride)
+    int32_t boff[MF_MAXT];                   // row offset of template entry t     (Σ off·bstride)
+    uint32_t mlo[3][2 * MF_R + 2], mhi[3][2 * MF_R + 2];   // template validity masks by edge class (MF_R)
+    int32_t loff[MF_MAXT];                   // A·v: LDS offset of template t (MfGrid bands)
+    int32_t wconst, var;                     // 1: every row of the part has row scale w; 1: field-valued
     double w;
-    double val[8];
+    double val[MF_MAXT];
+    int32_t fsel[MF_MAXT];                   // field-valued parts: field of template t
+    int32_t nfield, pad2;
+    const double* F;                         // field-valued parts: nfield × n_eq (device)
 };
 struct MfGrid {
     int32_t ndim, nparts;
@@ -190,6 +199,21 @@ struct NsTable {
         return coef.data() + ((size_t)(cy * ncls[1] + cx) * ncls[2] + ct) * offs.size();
     }
 };
+// A field-valued part on a 2-D grid as the CGNR normal operator applies it (k_cg_var2d): tiles of
+// CGV_TY × CGV_TX nodes; t = w·A_v p at the centres of a tile and its halo, q += w·A_vᵀ t and
+// Σ t² over the tile's own centres (= pᵀA_vᵀA_v p: each row lives in one tile).
+constexpr int CGV_TY = 8, CGV_TX = 64;
+struct CgVar {
+    int32_t S0, S1, col0, ntpl;
+    int32_t lo0, hi0, lo1, hi1;              // centre box (dims 0, 1)
+    int32_t nty, ntx, blk0, nfield;          // tiles; first partial slot of this part
+    int32_t R, pad;                          // template half-width (1 or 2)
+    int32_t oy[MF_MAXT], ox[MF_MAXT], fsel[MF_MAXT];
+    double val[MF_MAXT];
+    double w;
+    int64_t n_eq;
+    const double* F;
+};
 struct MgHier;   // multigrid hierarchy (mg.inc)
 void mg_free(MgHier* h);
 struct CgDesc {
@@ -245,6 +269,18 @@ struct System {
     bool rs_dirty = true;
     Sell A, AT;
     bool sell_built = false;   // A / AT exist (built lazily when the stencil operator is active)
+
+    // field-valued stencil parts (lsq_set_stencil_fields): staged by stencil index before the
+    // structured formation; the device fields live as long as the matrix (MfPart::F)
+    struct StencilFields {
+        int32_t stencil = -1, ntpl = 0, nfield = 0;
+        int32_t off[MF_MAXT][3] = {};
+        double val[MF_MAXT] = {};
+        int32_t fsel[MF_MAXT] = {};
+        DBuf<double> F;
+    };
+    std::vector<StencilFields> sfields;
+    bool has_var = false;      // the formed operator has field-valued parts
 
     // structured stencil operator (see MfDesc)
     bool mf = false;
@@ -321,6 +357,8 @@ struct System {
     DBuf<CgDesc> cgd;
     DBuf<double> cg_coef, cg_coefc;  // class-row tables: offset-major (tile mode), group × t (column mode)
     std::vector<NsTable> cg_ns;      // host copy of each grid's normal-stencil table (multigrid input)
+    std::vector<CgVar> cg_var;       // field-valued parts (k_cg_var2d), partial slots after the x-edge pass
+    int cg_nvb = 0;                  // their workgroups (partial slots)
     MgHier* mg = nullptr;            // precond 4: geometric multigrid levels (mg.inc), built lazily
     std::string mg_why;              // why precond 4 is unavailable
     std::vector<double> cg_wkey;   // part row scales the table was built for

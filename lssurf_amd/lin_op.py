@@ -258,6 +258,34 @@ class lin_op:
         self.__update_size_and_shape__()
         return self
 
+    def scale_rows(self, f):
+        """v[:, col] *= f for every template column (per-row scale of a stencil operator; what
+        notebooks/smooth_fit_demo_aniso.ipynb cell 9 does with the interpolated direction field).
+        Stencil parts keep their structure: the scale joins the part's value chain."""
+        f = np.asarray(f, dtype=float).ravel()
+        return self._chain(('rows', f), lambda V: V * f[:, None] if V.ndim > 1 else V * f)
+
+    def scale_values(self, c):
+        """v *= c (a scalar; notebook cell 10's ``temp.v *= 2``), keeping the stencil structure."""
+        c = float(c)
+        return self._chain(('const', c), lambda V: V * c)
+
+    def _chain(self, step, apply):
+        if self.parts is not None and all(p['kind'] == 'stencil' and p['row0'] == 0 and p['n_eq'] == self.N_eq
+                                          for p in self.parts):
+            f = self._lazy if self._lazy is not None else (lambda a=(self._r, self._c, self._v, self._ind0): a)
+
+            def build(f=f):
+                r, c, v, i0 = f()
+                return r, c, apply(v), i0
+            self._lazy = build
+            self.parts = [dict(p, chain=list(p.get('chain', [])) + [step]) for p in self.parts]
+        else:
+            self._materialize()
+            self._v = apply(self._v)
+            self.parts = None
+        return self
+
     def _stack_named(self, parts):
         subops = [lin_op(self.grid, name=nm).diff_op(subs, coeffs) for nm, subs, coeffs in parts]
         return self.vstack(tuple(subops))

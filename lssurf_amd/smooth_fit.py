@@ -65,11 +65,11 @@ class FitSystem:
         self.solver = LSQSolver(device)
         self.solver.set_col_map(self.n_full, keep_cols)
         m = self.n_data + self.n_con
-        desc = describe(G_data, Gc) if structured else None
+        desc = describe(G_data, Gc, with_fields=True) if structured else None
         self.formation = 'stencil' if desc is not None else 'coo'
         if desc is not None:       # rows generated on the device from the grids and stencils
-            gdesc, interp, coords, stencils, npts = desc
-            self.solver.set_matrix_stencil(m, self.n_full, gdesc, interp, coords, stencils, npts)
+            gdesc, interp, coords, stencils, npts, fields = desc
+            self.solver.set_matrix_stencil(m, self.n_full, gdesc, interp, coords, stencils, npts, fields=fields)
         else:                      # generic lin_op: host triplets -> device CSR
             r1, c1, v1 = G_data.triplets()
             r2, c2, v2 = Gc.triplets()

@@ -68,9 +68,15 @@ class LSQSolver:
             self.n = int(n_full)
         self.n_full = int(n_full)
 
-    def set_matrix_stencil(self, m, n_full, grids, interp_grid, coords, stencils, npts, row_weight=None):
-        """Structured formation (lssurf_amd.assemble.describe output) — rows generated on device."""
+    def set_matrix_stencil(self, m, n_full, grids, interp_grid, coords, stencils, npts, row_weight=None, fields=()):
+        """Structured formation (lssurf_amd.assemble.describe output) — rows generated on device.
+        fields: field-valued parts [(stencil index, off (ntpl×3), val, fsel, F (nfield × n_eq))]."""
         from ._native import GridDesc, StencilDesc
+        for k, off, val, fsel, F in fields:
+            off, val = as_c(off, np.int32).reshape(-1, 3), as_c(val, np.float64)
+            fsel, F = as_c(fsel, np.int32), as_c(F, np.float64)
+            self._check(self._L.lsq_set_stencil_fields(self._h, int(k), off.shape[0], ptr(off), ptr(val), F.shape[0],
+                                                       ptr(fsel), F.shape[1], ptr(F)), 'lsq_set_stencil_fields')
         ga = (GridDesc * len(grids))(*grids)
         sa = (StencilDesc * max(len(stencils), 1))(*stencils)
         ig = as_c(np.asarray(interp_grid, dtype=np.int32), np.int32)

@@ -27,7 +27,13 @@ CONFIGS = {
     # the per-rank compute floor of the strong-scaling runs, measurable on one GPU
     'c4y4': (1024, 12, 500_000, 258),
     'c4y8': (1024, 12, 250_000, 130),
+    # anisotropic-constraint systems (BASELINE config C5: lssurf_amd.aniso.system3d — the z0
+    # constraints are the notebook's directional operator along a circular field + magnitude)
+    'c5a': (2048, 12, 8_000_000),
+    'ta64': (64, 12, 8_192),
+    'ta100': (100, 8, 20_000),     # two dim-1 tiles of k_cg_var2d, 13 tile rows
 }
+ANISO = ('c5a', 'ta64', 'ta100')
 
 
 def config_kwargs(name, stiff=False):
@@ -87,3 +93,12 @@ def system2d(name):
     E_all = np.concatenate([sigma, g2.expected, g1.expected])
     rhs = np.concatenate([z, np.zeros(Gc.N_eq)])
     return G, Gc, g, 1. / E_all, rhs
+
+
+def aniso_system(name, stiff=False):
+    """lssurf_amd.aniso.system3d on the synthetic points of an anisotropic config (ANISO)."""
+    from . import aniso
+    D, kw = points(name)
+    if stiff:
+        kw['E_RMS'] = dict(E_RMS_STIFF)
+    return aniso.system3d(D, **kw), kw

@@ -98,6 +98,16 @@ class _PcGrid(_PcData):
         return out
 
 
+class _PcGridRBS(_PcGrid):
+    def interp(self, x, y, gridded=False, field='z'):
+        """pointCollection.grid.data.interp for the anisotropic notebook's direction field: a
+        bilinear RectBivariateSpline (kx = ky = 1) evaluated at the points (y, x)."""
+        from scipy.interpolate import RectBivariateSpline
+        z = np.asarray(getattr(self, field), float)
+        f = RectBivariateSpline(np.asarray(self.y, float), np.asarray(self.x, float), z, kx=1, ky=1)
+        return f.ev(np.asarray(y, float), np.asarray(x, float))
+
+
 def install():
     """Install the stubs and register the compiled reference kernels; returns LSsurf."""
     if not os.path.isdir(REF):

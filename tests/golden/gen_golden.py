@@ -20,6 +20,9 @@ tri.npz        I/O of the reference Cython kernels inv_tr_upper / propagate_qz_e
                spsolve_tr_upper on random upper-triangular CSR matrices (incl. overflow)
 sys_avg.npz    averaging products (avg_scales, z0_average_scale, avg_masks) and their errors
 kat.npz        the analytic amplitude KAT of notebooks/smooth_fit_demo.ipynb cell 8
+sys_aniso*.npz notebooks/smooth_fit_demo_aniso.ipynb's directional-smoothing systems (the notebook's
+               own cells 8-10 and 15 executed from the notebook file on the reference LSsurf): the
+               2-D notebook system at 41² / 37² and the C5 z0 + dz system at toy size
 """
 import os
 import sys
@@ -263,6 +266,110 @@ def gen_lin2d(LS):
     print(f'lin2d: A {A.shape} nnz {A.nnz}, opt {out["x_opt"]:.2e}')
 
 
+NB_ANISO = '/root/reference/notebooks/smooth_fit_demo_aniso.ipynb'
+
+
+def _notebook_ns(LS, stubs):
+    """Execute the anisotropic notebook's own definitions (cells 8-10: make_system_of_ops,
+    scale_op_by_2d_grid, directional_smoothing_op) and its circular direction field (cell 15)
+    from the reference notebook file, against the reference LSsurf.  The field's container is
+    the stub grid whose interp is pointCollection's bilinear RectBivariateSpline."""
+    import json
+    import types
+    cells = [c for c in json.load(open(NB_ANISO))['cells'] if c['cell_type'] == 'code']
+    src = {i: ''.join(c['source']) for i, c in enumerate(cells)}
+    need = [k for k, s in src.items() if 'def make_system_of_ops' in s or 'def scale_op_by_2d_grid' in s
+            or 'def directional_smoothing_op' in s]
+    field = [k for k, s in src.items() if 'velocity field going around in a circle' in s]
+    assert len(need) == 3 and len(field) == 1, 'notebook layout changed'
+    plt = types.SimpleNamespace(figure=lambda *a, **k: None, quiver=lambda *a, **k: None)
+    pcns = types.SimpleNamespace(data=stubs._PcData, grid=types.SimpleNamespace(data=stubs._PcGridRBS))
+    ns = {'np': np, 'LSsurf': LS, 'sp': sp, 'pc': pcns, 'plt': plt}
+    for k in need + field:
+        exec(compile(src[k], f'{NB_ANISO}:cell{k}', 'exec'), ns)
+    return ns
+
+
+def _u_arrays(u, prefix='u'):
+    return {prefix + '_x': np.asarray(u.x), prefix + '_y': np.asarray(u.y), prefix + '_u': np.asarray(u.u),
+            prefix + '_v': np.asarray(u.v)}
+
+
+def gen_aniso(LS, stubs):
+    """notebooks/smooth_fit_demo_aniso.ipynb (BASELINE C5's constraint), run on the reference:
+    (1) the 2-D notebook system of cells 13-18 (directional operator along the circular field,
+    E = 0.25, magnitude constraint expected 2) at reduced grid sizes — 41² (every z0 node on a
+    field node) with the notebook's eight points, 37² (interpolated field) with seeded points;
+    (2) the C5 system at toy size: smooth_fit's z0 + dz system (return_fit_objects) with the z0
+    constraints replaced by the directional operator and the magnitude constraint, Ip_c and TCinv
+    as smooth_fit.py:613-627 form them.  Each: A, b handed to sparseqr.solve, exact x*."""
+    from oracle import dense
+    import pointCollection as pc
+    ns = _notebook_ns(LS, stubs)
+    u = ns['u']
+    rng = np.random.default_rng(20251123)
+    for n, npts in ((41, 0), (37, 300)):
+        g = LS.fd_grid([[-10., 10.], [-10., 10.]], (20. / (n - 1)) * np.ones(2))
+        if npts:
+            x, y = rng.uniform(-10, 10, npts), rng.uniform(-10, 10, npts)
+            z = 10 * np.sin(2 * np.pi * x / 10) * np.cos(2 * np.pi * y / (20 / 3)) + rng.normal(0, 0.1, npts)
+        else:   # cell 18
+            pts = 5 * np.exp(1j * np.arange(0, 2 * np.pi, np.pi / 4))
+            x, y, z = np.real(pts), np.imag(pts), np.ones(pts.shape)
+        sigma = 0.1 * np.ones(x.size)
+        G_data = LS.lin_op(g, name='interp_z').interp_mtx([y, x])
+        Axy = ns['directional_smoothing_op'](g, u)
+        Axy.expected = 0.25 + np.zeros(Axy.shape[0])
+        mag = LS.lin_op(g, name='mag_z0').one(DOF='z0')
+        mag.expected = 2 + np.zeros(mag.N_eq)
+        Gc = LS.lin_op(None, name='constraints').vstack([Axy, mag])
+        Gcoo = sp.vstack([G_data.toCSR(), Gc.toCSR()]).tocoo()
+        E = np.concatenate([sigma, Axy.expected.ravel(), mag.expected.ravel()])
+        rhs = np.concatenate([z, np.zeros([Gc.shape[0]])], axis=0)
+        TCinv = sp.dia_matrix((1 / E, 0), shape=(rhs.size, rhs.size))
+        A, b = TCinv.dot(Gcoo), TCinv.dot(rhs)
+        xs = dense.ls_solve_dense(A, b)
+        out = {'in_x': x, 'in_y': y, 'in_z': z, 'nodes': np.array(n), 'b': b, 'x': xs,
+               'x_opt': np.array(dense.optimality(A, b, xs)), **_u_arrays(u)}
+        out.update(_csr_arrays('A', A))
+        out.update(_csr_arrays('Axy', Axy.toCSR()))
+        np.savez_compressed(os.path.join(HERE, f'sys_aniso{n}.npz'), **out)
+        print(f'aniso{n}: A {A.shape} nnz {A.nnz}, opt {out["x_opt"]:.2e}')
+    # (2) C5 at toy size
+    from LSsurf.constraint_functions import build_reference_epoch_matrix
+    W = {'x': 1500., 'y': 1500., 't': 1.25}
+    ctr = {'x': 0., 'y': 0., 't': 0.}
+    x, y, t, z = synth_points(rng, W, ctr, 900)
+    E_dz = {k: v for k, v in E_RMS_NB.items() if k not in ('d2z0_dx2', 'dz0_dx')}
+    F = LS.smooth_fit(data=pc.data().from_dict({'x': x, 'y': y, 'time': t, 'z': z, 'sigma': np.full(x.size, 0.1)}),
+                      W=W, ctr=ctr, spacing={'z0': 100., 'dz': 100., 'dt': 0.25}, E_RMS=E_dz, reference_epoch=2,
+                      return_fit_objects=True, VERBOSE=False)
+    grids = F['grids']
+    u3 = stubs._PcGridRBS().from_dict({'x': u.x * 75., 'y': u.y * 75., 'u': u.u, 'v': u.v})   # [-750, 750]²
+    Axy = ns['directional_smoothing_op'](grids['z0'], u3)
+    Axy.expected = E_RMS_NB['d2z0_dx2'] / np.sqrt(np.prod(grids['z0'].delta)) + np.zeros(Axy.shape[0])
+    mag = LS.lin_op(grids['z0'], name='mag_z0').one(DOF='z0')
+    mag.expected = 2 + np.zeros(mag.N_eq)
+    Gc = LS.lin_op(None, name='constraints').vstack([Axy, mag, F['Gc']])
+    Ec = np.concatenate([Axy.expected, mag.expected, F['Ec']])
+    Ed = F['Ed']
+    N_eq = F['G_data'].N_eq + Gc.N_eq
+    TCinv = sp.dia_matrix((1. / np.concatenate((Ed, Ec)), 0), shape=(N_eq, N_eq))
+    rhs = np.zeros([N_eq])
+    rhs[0:F['data'].size] = F['data'].z.ravel()
+    Gcoo = sp.vstack([F['G_data'].toCSR(), Gc.toCSR()]).tocoo()
+    Ip_c = build_reference_epoch_matrix(F['G_data'], Gc, grids, 2)
+    A, b = TCinv.dot(Gcoo.dot(Ip_c)), TCinv.dot(rhs)
+    xs = dense.ls_solve_dense(A, b)
+    out = {'in_x': x, 'in_y': y, 'in_time': t, 'in_z': z, 'in_sigma': np.full(x.size, 0.1), 'b': b, 'x': xs,
+           'x_opt': np.array(dense.optimality(A, b, xs)), 'u_scale': np.array(75.), **_u_arrays(u),
+           'kwargs': np.array(repr(dict(W=W, ctr=ctr, spacing={'z0': 100., 'dz': 100., 'dt': 0.25}, E_RMS=E_RMS_NB,
+                                         reference_epoch=2)))}
+    out.update(_csr_arrays('A', A))
+    np.savez_compressed(os.path.join(HERE, 'sys_aniso3d.npz'), **out)
+    print(f'aniso3d: A {A.shape} nnz {A.nnz}, opt {out["x_opt"]:.2e}')
+
+
 def rand_upper(rng, N, density, diag_first=True):
     R = sp.random(N, N, density=density, random_state=rng, format='csr')
     R = sp.triu(R, k=1).tocsr()
@@ -337,12 +444,11 @@ def main():
     import _refstubs
     LS = _refstubs.install()
     sys.modules['LSsurf.smooth_fit'].smooth_fit   # module (LSsurf/__init__.py:6 rebinds the name)
-    gen_stencils(LS)
-    gen_tri(LS)
-    gen_lin2d(LS)
-    gen_systems(LS, _refstubs)
-    gen_avg(LS, _refstubs)
-    gen_kat(LS)
+    gens = {'stencils': lambda: gen_stencils(LS), 'tri': lambda: gen_tri(LS), 'lin2d': lambda: gen_lin2d(LS),
+            'systems': lambda: gen_systems(LS, _refstubs), 'avg': lambda: gen_avg(LS, _refstubs),
+            'kat': lambda: gen_kat(LS), 'aniso': lambda: gen_aniso(LS, _refstubs)}
+    for name in (sys.argv[1:] or list(gens)):   # e.g. `gen_golden.py aniso`: only those fixtures
+        gens[name]()
 
 
 if __name__ == '__main__':
