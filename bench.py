@@ -22,6 +22,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+ANISO = ('c5a', 'ta64', 'ta100')   # lssurf_amd.synthetic.ANISO (no package import before the PMC passes)
 
 
 def log(*a):
@@ -35,6 +36,13 @@ def build_system(config, device):
     from lssurf_amd.constraint_functions import reference_epoch_keep_cols
     from lssurf_amd.smooth_fit import FitSystem
     t0 = time.time()
+    if config in synthetic.ANISO:   # BASELINE C5: the directional (anisotropic) z0 constraint
+        S, kw = synthetic.aniso_system(config)
+        t1 = time.time()
+        fs = FitSystem(S['G_data'], S['Gc'], S['keep'], S['Gc'].col_N, device=device, grids=S['grids'])
+        fs.solver.set_row_weight(S['w'])
+        fs.solver.set_row_mask(np.ones(S['w'].size, bool))
+        return fs, S['rhs'], S['w'], {'host_assembly_s': t1 - t0, 'device_formation_s': time.time() - t1}
     if config in synthetic.CONFIGS_2D:   # 2-D z0-only lin_op system (BASELINE C2), structured formation
         G, Gc, grid, w, rhs = synthetic.system2d(config)
         t1 = time.time()
@@ -212,6 +220,8 @@ def main():
     ap.add_argument('--cpu-iters', type=int, default=80,
                     help='LSQR iterations of the CPU baseline sample (~11 s on 16 host threads at C4)')
     ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--cpu-solve', action='store_true',
+                    help='also run the CPU oracle LSQR to the solve tolerance (BASELINE.md §4 parity at size; slow)')
     ap.add_argument('--dist', action='store_true', help='use the distributed (RCCL) path even at N=1')
     ap.add_argument('--no-pmc', action='store_true', help='skip the rocprofv3 PMC traffic passes')
     ap.add_argument('--op', type=int, default=0, help='0: auto (structured stencil operator), 1: assembled SELL')
@@ -321,8 +331,17 @@ def main():
             sp = 4
 
         def rec(st):
+            # solve_time_s: device iterations; solve_setup_s: the per-solve preconditioner set-up
+            # (block factors / multigrid levels, λ estimates) that every solve pays; total = both
             return {'solve_time_s': st['time_s'], 'solve_setup_s': st.get('setup_s', 0.0),
-                    'solve_iters': int(st['iters']), 'solve_istop': int(st['istop'])}
+                    'solve_total_s': st['time_s'] + st.get('setup_s', 0.0),
+                    'solve_iters': int(st['iters']), 'solve_istop': int(st['istop']),
+                    'solve_iters_per_s': st['iters'] / st['time_s'] if st['time_s'] > 0 else None,
+                    'solve_roofline': {'bytes_per_iter': st['bytes_per_iter'],
+                                       'achieved_gbs': st['bytes_per_iter'] * st['iters'] / st['time_s'] / 1e9
+                                       if st['time_s'] > 0 else None,
+                                       'frac': st['bytes_per_iter'] * st['iters'] / st['time_s'] / 1e9 / HBM_PEAK_GBS
+                                       if st['time_s'] > 0 else None}}
         x, sst = solver.solve(rhs, op=args.op, precond=sp, method=meth)
         solve = dict(rec(sst), solve_method=['lsqr', 'cgnr'][int(sst.get('method', 0))],
                      solve_precond=names.get(sp, sp))
@@ -333,12 +352,21 @@ def main():
                 solve['solve_rel_diff_vs_block_jacobi'] = float(np.linalg.norm(x - xb) / np.linalg.norm(xb))
             xl, sl = solver.solve(rhs, op=args.op, precond=min(args.precond, 3), method=0)
             solve['solve_lsqr'] = rec(sl)
+            solve['lsqr_iters_per_s'] = solve['solve_lsqr']['solve_iters_per_s']
             solve['solve_rel_diff_vs_lsqr'] = float(np.linalg.norm(x - xl) / np.linalg.norm(xl))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not args.dist:
         threads = min(os.cpu_count() or 1, 16)
         cpu = cpu_baseline(fs, w * rhs, args.cpu_iters, threads)
+        if args.cpu_solve and solve:   # the CPU oracle to the same stopping rule, on the same A, b
+            from oracle import cpu as ocpu
+            xc, stc = ocpu.lsqr(fs.solver.get_csr(), w * rhs, atol=1e-10, btol=1e-10, conlim=1e8,
+                                maxit=50 * int(info['n']), threads=threads)
+            cpu.update({'solve_time_s': stc['time_s'], 'solve_iters': int(stc['iters']),
+                        'solve_istop': int(stc.get('istop', -1)),
+                        'solve_rule': 'LSQR, column scaling, atol = btol = 1e-10 (the GPU solves\' rule)',
+                        'solve_rel_diff_gpu_vs_cpu': float(np.linalg.norm(x - xc) / np.linalg.norm(xc))})
     fs.close()
 
     traffic, traffic_note = (pmc[dom]['total'], pmc) if pmc else (None, pmc_note)
@@ -347,12 +375,14 @@ def main():
     if rank == 0:
         out = {
             'metric': 'LSQR iters/sec + solve wall-time, 1024x1024x12 grid / 2M pts, 1-8 GPU',
-            'value': value, 'unit': 'LSQR iters/s',
+            'value': value, 'unit': 'CGNR iters/s (block-Jacobi PCG on AᵀA = LSQR\'s iterates on A·M^-1/2)'
+                                    if meth == 1 else 'LSQR iters/s',
             'solver': method_name, 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': ms_per_step, 'higher_is_better': True,
             'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f64',
             'data': 'synthetic (SURVEY.md §8(d) point cloud)',
-            'config': {'workload': f'{"2-D lin_op (z0 only)" if args.config in ("c2", "t2d") else "smooth_fit"} solve, {args.config}',
+            'config': {'workload': f'{"2-D lin_op (z0 only)" if args.config in ("c2", "t2d") else "smooth_fit"} solve, {args.config}'
+                                   + (' (directional z0 constraint, aniso notebook)' if args.config in ANISO else ''),
                        'rank0_system': info, 'rows': gm, 'cols': gn,
                        'nnz': gZ, 'precond': {1: 'column scaling', 3: 'block-Jacobi per (y,x) node'}.get(args.precond, args.precond),
                        'operator': ('structured stencil rows + ' + ('matrix-free data rows (points sorted by cell)'

@@ -24,8 +24,10 @@
  *     device memory.  Pointers are plain host pointers, sizes are int64.
  *   - Errors: int return, 0 = ok, 1 = "not converged" (lsq_solve hit maxit) or "output buffer
  *     full" (tri_upper_inv_csr, same meaning as inv_tr_upper's status=1); < 0 = invalid
- *     argument / call order / HIP error, with lsq_last_error() describing it.  There is no CPU
- *     fallback: without a usable gfx950 device every call fails.
+ *     argument / call order / HIP error, with lsq_last_error() describing it; -5 = declined for
+ *     lack of resources (a band factor that does not fit the device or exceeds the width limit —
+ *     the caller may choose another preconditioner).  There is no CPU fallback: without a
+ *     usable gfx950 device every call fails.
  *   - Threading: one handle per host thread; calls on one handle are serialised.
  */
 #ifndef LSQSURF_H

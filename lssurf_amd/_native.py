@@ -13,6 +13,11 @@ class NativeError(RuntimeError):
     pass
 
 
+class NativeRefused(NativeError):
+    """Status -5: declined for lack of resources (include/lsqsurf.h); another method may run."""
+    pass
+
+
 class LsqOpts(ctypes.Structure):
     _fields_ = [('method', ctypes.c_int32), ('precond', ctypes.c_int32), ('atol', ctypes.c_double),
                 ('btol', ctypes.c_double), ('conlim', ctypes.c_double), ('maxit', ctypes.c_int64),

@@ -38,6 +38,9 @@ int guarded(lsq_handle* h, F&& f) {
     try {
         HIP_CHECK(hipSetDevice(h->sys.device));
         return f(h->sys);
+    } catch (const lsq::Refused& e) {
+        h->sys.err = e.what();
+        return -5;
     } catch (const std::invalid_argument& e) {
         h->sys.err = e.what();
         return -2;

@@ -233,14 +233,17 @@ bool describe_stencil_operator(MfDesc& d, int64_t m, int64_t n_full, int32_t n_g
         // a = clamp(c - lo + MF_R + 1, 0, 2 MF_R + 1) and b = clamp(c - hi + MF_R + 1, ...):
         // mlo[k][a] / mhi[k][b] hold the templates valid on that side (bit t).
         for (int k = 0; k < 3; ++k) {
+            P.mlo[k][0] = P.mlo[k][1] = P.mhi[k][0] = P.mhi[k][1] = P.mlo8[k] = P.mhi8[k] = 0;
             for (int a = 0; a <= 2 * MF_R + 1; ++a) {
-                uint32_t lo_bits = 0, hi_bits = 0;
+                uint64_t lo_bits = 0, hi_bits = 0;
                 for (int t = 0; t < S.ntpl; ++t) {
-                    if (P.off[t][k] <= a - MF_R - 1) lo_bits |= 1u << t;
-                    if (P.off[t][k] >= a - MF_R) hi_bits |= 1u << t;
+                    if (P.off[t][k] <= a - MF_R - 1) lo_bits |= uint64_t(1) << t;
+                    if (P.off[t][k] >= a - MF_R) hi_bits |= uint64_t(1) << t;
                 }
-                P.mlo[k][a] = lo_bits;
-                P.mhi[k][a] = hi_bits;
+                P.mlo[k][a >> 2] |= lo_bits << (16 * (a & 3));
+                P.mhi[k][a >> 2] |= hi_bits << (16 * (a & 3));
+                P.mlo8[k] |= (lo_bits & 0xFF) << (8 * a);
+                P.mhi8[k] |= (hi_bits & 0xFF) << (8 * a);
             }
         }
         G.part[G.nparts++] = d.n_parts++;

@@ -787,7 +787,7 @@ void band_factor(System& S, const int32_t* h_perm, BandFactor& F) {
     size_t free_b = 0, total_b = 0;
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
     if ((double)bytes > 0.85 * (double)free_b)
-        throw std::invalid_argument("band factor: a band of " + std::to_string(w) + " tiles needs " +
+        throw Refused("band factor: a band of " + std::to_string(w) + " tiles needs " +
                                     std::to_string(bytes >> 20) + " MiB, more than the device has free");
     F.valid = false;
     F.n = n;
@@ -848,7 +848,7 @@ void band_precond(System& S) {
     band_factor(S, S.band_order.empty() ? nullptr : S.band_order.data(), S.band);
     if (S.band.w > BAND_PRECOND_WMAX) {
         S.band.valid = false;
-        throw std::invalid_argument("precond 5: the band of AᵀA is " + std::to_string(S.band.w) +
+        throw Refused("precond 5: the band of AᵀA is " + std::to_string(S.band.w) +
                                     " tiles wide (at most " + std::to_string(BAND_PRECOND_WMAX) +
                                     "); set a bandwidth-reducing order (lsq_set_band_order)");
     }
@@ -941,7 +941,7 @@ void band_cov(System& S, const int32_t* h_perm, double* h_E, int64_t nops, const
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
     const double avail = 0.9 * (double)free_b;
     if (avail < (double)ring_wg * 64)
-        throw std::invalid_argument("lsq_cov_band: no device memory left for the sweeps of a " + std::to_string(w) +
+        throw Refused("lsq_cov_band: no device memory left for the sweeps of a " + std::to_string(w) +
                                     "-tile band");
     // rings for up to `cap` concurrent workgroups (launches are batched beyond)
     const int64_t nop_wg = (nops + TB - 1) / TB;

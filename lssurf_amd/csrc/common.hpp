@@ -17,6 +17,11 @@ constexpr int MAX_GRID = 2048;    // 256 CUs x 8 resident 256-thread blocks (Gui
 struct HipError : std::runtime_error {
     using std::runtime_error::runtime_error;
 };
+// A request the library declines for lack of resources (device memory, band width): status -5,
+// so a caller may fall back to another method instead of failing (everything else is an error).
+struct Refused : std::invalid_argument {
+    using std::invalid_argument::invalid_argument;
+};
 
 #define HIP_CHECK(expr)                                                                     \
     do {                                                                                    \

@@ -486,20 +486,20 @@ void launch_iteration_mf(System& S, const Grids& g, int p, int precond) {
     hipStream_t st = S.stream;
     double* vt = p ? S.vb1.p : S.vb0.p;
     double* vo = p ? S.vb0.p : S.vb1.p;
-    hipLaunchKernelGGL(k_mf_fwd, dim3(g.gXf + g.gD + g.gS), dim3(BLOCK), g.lds, st, S.st.p, g.gXf, g.gD, S.n_full, S.y.p,
+    hipLaunchKernelGGL(k_mf_fwd_for(S), dim3(g.gXf + g.gD + g.gS), dim3(BLOCK), g.lds, st, S.st.p, g.gXf, g.gD, S.n_full, S.y.p,
                        S.w.p, vt, S.mfh.npts, S.Ad.nslices, S.Ad.sp.p, S.Ad.ci.p, S.Ad.val.p, S.mfd.p, S.zv.p, S.rs.p,
                        S.u.p, S.part_u.p, S.part_w.p);
     hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gD + g.gS, S.part_b.p, 0, 0,
                        nullptr);
     if (precond == 3) {   // raw Aᵀũ, then ṽ' = M^T t/β − βṽ/α and zv = M ṽ' per column block
-        hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.rp.p, S.ATd.ci.p, S.ATd.val.p,
+        hipLaunchKernelGGL(k_mf_spmtv_for(S), dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.rp.p, S.ATd.ci.p, S.ATd.val.p,
                            S.mfd.p, S.u.p, S.rs.p, S.csf.p, vt, S.tt.p, S.zv.p, S.part_v.p, 1);
         launch_block_epi(S, true, g.gB, S.tt.p, vt, vo, S.zv.p);
         hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gB, S.part_w.p, g.gXf, 0,
                            nullptr);
         return;
     }
-    hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.rp.p, S.ATd.ci.p, S.ATd.val.p,
+    hipLaunchKernelGGL(k_mf_spmtv_for(S), dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.rp.p, S.ATd.ci.p, S.ATd.val.p,
                        S.mfd.p, S.u.p, S.rs.p, S.csf.p, vt, vo, S.zv.p, S.part_v.p, 0);
     hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gM, S.part_w.p, g.gXf, 0, nullptr);
 }
@@ -507,7 +507,7 @@ void launch_iteration_mf(System& S, const Grids& g, int p, int precond) {
 // final x/w update of a solve that stopped on the last iteration of a batch (newest ṽ in vb0)
 void launch_flush(System& S, const Grids& g, bool mf) {
     if (mf) {
-        hipLaunchKernelGGL(k_mf_fwd, dim3(g.gXf + g.gD + g.gS), dim3(BLOCK), g.lds, S.stream, S.st.p, g.gXf, g.gD,
+        hipLaunchKernelGGL(k_mf_fwd_for(S), dim3(g.gXf + g.gD + g.gS), dim3(BLOCK), g.lds, S.stream, S.st.p, g.gXf, g.gD,
                            S.n_full, S.y.p, S.w.p, S.vb0.p, S.mfh.npts, S.Ad.nslices, S.Ad.sp.p, S.Ad.ci.p, S.Ad.val.p,
                            S.mfd.p, S.zv.p, S.rs.p, S.u.p, S.part_u.p, S.part_w.p);
         hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, S.stream, S.st.p, S.part_u.p, g.gD + g.gS, S.part_b.p, 0, 0,
@@ -561,7 +561,7 @@ void lsqr_init_mf(System& S, const double* h_b, const double* h_x0, const lsq_op
     h.no_stop = no_stop ? 1 : 0;
     h.cs2 = -1.0;
     HIP_CHECK(hipMemcpyAsync(S.st.p, &h, sizeof(h), hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_mf_init_u, dim3(g.gD + g.gS), dim3(BLOCK), 0, st, g.gD, S.mfh.npts, S.Ad.nslices, S.Ad.sp.p,
+    hipLaunchKernelGGL(k_mf_init_u_for(S), dim3(g.gD + g.gS), dim3(BLOCK), 0, st, g.gD, S.mfh.npts, S.Ad.nslices, S.Ad.sp.p,
                        S.Ad.ci.p, S.Ad.val.p, S.Ad.perm.p, S.mfd.p, h_x0 ? dz0.p : nullptr, S.rs.p, db.p, S.u.p, S.bw.p,
                        S.part_u.p, S.part_b.p);
     KERNEL_CHECK();
@@ -571,13 +571,13 @@ void lsqr_init_mf(System& S, const double* h_b, const double* h_x0, const lsq_op
     if (o.precond == 3) {
         S.vb0.zero(st);   // columns outside every block (removed by Ip_c) stay 0
         S.zv.zero(st);
-        hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.rp.p, S.ATd.ci.p, S.ATd.val.p,
+        hipLaunchKernelGGL(k_mf_spmtv_for(S), dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.rp.p, S.ATd.ci.p, S.ATd.val.p,
                            S.mfd.p, S.u.p, S.rs.p, S.csf.p, S.vb1.p, S.tt.p, S.zv.p, S.part_v.p, 1);
         launch_block_epi(S, true, g.gB, S.tt.p, S.vb1.p, S.vb0.p, S.zv.p);
         hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gB, S.part_w.p, g.gXf, 1,
                            nullptr);
     } else {
-        hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.rp.p, S.ATd.ci.p, S.ATd.val.p,
+        hipLaunchKernelGGL(k_mf_spmtv_for(S), dim3(g.gM), dim3(BLOCK), 0, st, S.st.p, S.ATd.rp.p, S.ATd.ci.p, S.ATd.val.p,
                            S.mfd.p, S.u.p, S.rs.p, S.csf.p, S.vb1.p, S.vb0.p, S.zv.p, S.part_v.p, 0);
         hipLaunchKernelGGL(k_givens, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_v.p, g.gM, S.part_w.p, g.gXf, 1,
                            nullptr);
@@ -919,7 +919,7 @@ void lsqr_profile(System& S, int reps, int op, double* out /* [8] */) {
             HIP_CHECK(hipEventRecord(e0, S.stream));
             for (int r = 0; r < reps; ++r) {
                 if (k == 0 && mf)
-                    hipLaunchKernelGGL(k_mf_fwd, dim3(g.gXf + g.gD + g.gS), dim3(BLOCK), g.lds, S.stream, S.st.p, g.gXf,
+                    hipLaunchKernelGGL(k_mf_fwd_for(S), dim3(g.gXf + g.gD + g.gS), dim3(BLOCK), g.lds, S.stream, S.st.p, g.gXf,
                                        g.gD, S.n_full, S.y.p, S.w.p, S.vb0.p, S.mfh.npts, S.Ad.nslices, S.Ad.sp.p,
                                        S.Ad.ci.p, S.Ad.val.p, S.mfd.p, S.zv.p, S.rs.p, S.u.p, S.part_u.p, S.part_w.p);
                 else if (k == 0)
@@ -927,7 +927,7 @@ void lsqr_profile(System& S, int reps, int op, double* out /* [8] */) {
                                        S.y.p, S.w.p, S.vb0.p, S.vb0.p, 1, S.G.m, S.A.nslices, S.A.sp.p, S.A.ci.p,
                                        S.A.val.p, S.u.p, S.part_u.p, S.part_w.p);
                 else if (k == 1 && mf)
-                    hipLaunchKernelGGL(k_mf_spmtv, dim3(g.gM), dim3(BLOCK), 0, S.stream, S.st.p, S.ATd.rp.p,
+                    hipLaunchKernelGGL(k_mf_spmtv_for(S), dim3(g.gM), dim3(BLOCK), 0, S.stream, S.st.p, S.ATd.rp.p,
                                        S.ATd.ci.p, S.ATd.val.p, S.mfd.p, S.u.p, S.rs.p, S.csf.p, S.vb0.p, S.vb1.p,
                                        S.zv.p, S.part_v.p, 0);
                 else if (k == 1)

@@ -85,7 +85,9 @@ struct MfPart {
     int32_t off[MF_MAXT][3];
     int32_t doff[MF_MAXT];                   // column offset of template entry t  (Σ off·stride)
     int32_t boff[MF_MAXT];                   // row offset of template entry t     (Σ off·bstride)
-    uint32_t mlo[3][2 * MF_R + 2], mhi[3][2 * MF_R + 2];   // template validity masks by edge class (MF_R)
+    uint64_t mlo8[3], mhi8[3];               // template validity masks by edge class (MF_R), ≤ 8 entries: byte a
+    uint64_t mlo[3][2], mhi[3][2];           // the same for ≤ 16 entries (field-valued parts): 16 bits per class,
+                                             // class a of dim e at bit 16·(a mod 4) of word a / 4 (mf_mask)
     int32_t loff[MF_MAXT];                   // A·v: LDS offset of template t (MfGrid bands)
     int32_t wconst, var;                     // 1: every row of the part has row scale w; 1: field-valued
     double w;

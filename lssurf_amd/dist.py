@@ -44,7 +44,8 @@ def rank_problem(G_data, Gc, partition, rank):
     """Descriptors of the rows `rank` owns + their global row ids (None: not structured)."""
     desc = assemble.describe(G_data, Gc)
     if desc is None:
-        raise NotImplementedError('distributed solve needs a structured (stencil + interp) system')
+        raise NotImplementedError('distributed solve on assembled ranks needs a constant-coefficient stencil system '
+                                  '(field-valued parts: structured ranks)')
     grid_descs, interp, (py, px, pt), stencils, npts = desc
     grid_objs = {}
     for p in list(G_data.parts) + list(Gc.parts):
@@ -81,7 +82,7 @@ def rank_problem(G_data, Gc, partition, rank):
 
 
 def _describe_order(G_data, Gc):
-    desc = assemble.describe(G_data, Gc)
+    desc = assemble.describe(G_data, Gc, with_fields=True)
     if desc is None:
         raise NotImplementedError('distributed solve needs a structured (stencil + interp) system')
     order, seen = [], set()
@@ -113,8 +114,10 @@ def window_problem(G_data, Gc, partition, rank, keep_cols):
     (own column numbering), the stencil parts clipped to its owned centre rows, its points, and
     the maps to the global system.  Every rank computes every window (no communication)."""
     from ._native import GridDesc
-    (grid_descs, interp, (py, px, pt), stencils, npts), order = _describe_order(G_data, Gc)
-    halo = max([1] + [abs(int(s.off[t][0])) for s in stencils for t in range(s.ntpl)])
+    (grid_descs, interp, (py, px, pt), stencils, npts, fields), order = _describe_order(G_data, Gc)
+    fields = {f[0]: f for f in fields}            # field-valued parts by stencil index
+    halo = max([1] + [abs(int(s.off[t][0])) for k, s in enumerate(stencils) if k not in fields for t in range(s.ntpl)]
+               + [int(np.abs(f[1][:, 0]).max()) for f in fields.values()])
     meta, nloc = window_meta(order, partition, rank, halo)
     grids = []
     for gd, gm in zip(grid_descs, meta):
@@ -125,9 +128,9 @@ def window_problem(G_data, Gc, partition, rank, keep_cols):
         grids.append(d)
     pts_own = np.flatnonzero(partition.owner(py) == rank)
     rows = [pts_own]
-    local = []
+    local, local_fields = [], []
     row0 = pts_own.size
-    for s, part in zip(stencils, Gc.parts):
+    for k, s in enumerate(stencils):
         gm = meta[s.grid]
         lo_y, hi_y = max(int(s.lo[0]), gm['a']), min(int(s.hi[0]), gm['b'])
         if lo_y >= hi_y:
@@ -138,8 +141,12 @@ def window_problem(G_data, Gc, partition, rank, keep_cols):
         t.lo[0], t.hi[0] = lo_y - gm['wa'], hi_y - gm['wa']
         t.n_eq = (hi_y - lo_y) * inner
         t.row0 = row0
-        first = npts + int(part['row0']) + (lo_y - int(s.lo[0])) * inner
+        k0 = (lo_y - int(s.lo[0])) * inner            # first of the part's rows kept (centre order)
+        first = int(s.row0) + k0
         rows.append(first + np.arange(t.n_eq))
+        if k in fields:                               # the kept rows' field values
+            _, off, val, fsel, F = fields[k]
+            local_fields.append((len(local), off, val, fsel, np.ascontiguousarray(F[:, k0:k0 + t.n_eq])))
         row0 += t.n_eq
         local.append(t)
     coords = (py[pts_own].copy(), px[pts_own].copy(), None if pt is None else pt[pts_own].copy())
@@ -150,8 +157,8 @@ def window_problem(G_data, Gc, partition, rank, keep_cols):
     keep_local = np.flatnonzero(keep_cols[pos] == l2g)
     own_ranges = [(gm['col0'] + (gm['a'] - gm['wa']) * gm['stride'], gm['col0'] + (gm['b'] - gm['wa']) * gm['stride'])
                   for gm in meta]
-    return dict(grids=grids, grid_objs=order, interp=interp, coords=coords, stencils=local, npts=int(pts_own.size),
-                rows=np.concatenate(rows), m=int(row0), n_full=int(nloc), keep=keep_local, l2g=l2g,
+    return dict(grids=grids, grid_objs=order, interp=interp, coords=coords, stencils=local, fields=local_fields,
+                npts=int(pts_own.size), rows=np.concatenate(rows), m=int(row0), n_full=int(nloc), keep=keep_local, l2g=l2g,
                 keep_global=pos[keep_local], own_ranges=own_ranges, meta=meta, halo=halo)
 
 
@@ -191,6 +198,11 @@ def _form_window(L, h, prob):
     sa = (StencilDesc * max(len(prob['stencils']), 1))(*prob['stencils'])
     ig = as_c(np.asarray(prob['interp'], np.int32), np.int32)
     py, px, pt = prob['coords']
+    for k, off, val, fsel, F in prob.get('fields', ()):
+        off, val, fsel = as_c(off, np.int32).reshape(-1, 3), as_c(val, np.float64), as_c(fsel, np.int32)
+        F = as_c(F, np.float64)
+        s.check(L.lsq_set_stencil_fields(h, int(k), off.shape[0], ptr(off), ptr(val), F.shape[0], ptr(fsel), F.shape[1],
+                                         ptr(F)), 'lsq_set_stencil_fields')
     s.check(L.lsq_set_matrix_stencil(h, prob['m'], prob['n_full'], len(prob['grids']),
                                      ctypes.cast(ga, ctypes.c_void_p), len(prob['interp']), ptr(ig), prob['npts'],
                                      ptr(py), ptr(px), ptr(pt), len(prob['stencils']), ctypes.cast(sa, ctypes.c_void_p),

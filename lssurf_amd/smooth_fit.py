@@ -28,6 +28,7 @@ from .constraint_functions import build_reference_epoch_matrix, node_column_bloc
 from .grid_functions import setup_averaging_ops, setup_avg_mask_ops, setup_grids, setup_z0_avg, \
     validate_by_dz_mask
 from .lin_op import known_range, lin_op
+from ._native import NativeError
 from .assemble import describe
 from .solver import LSQSolver
 
@@ -188,7 +189,19 @@ def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grid
             system.multigrid_available(weight)
         if mg and 'mg_build' not in timing:
             timing['mg_build'] = system.mg_build_s
-        x = system.solve(weight, in_TSE, rhs, x0=x0, **_solve_opts(args, system.keep_cols.size, system.has_blocks, mg))
+        opts = _solve_opts(args, system.keep_cols.size, system.has_blocks, mg)
+        try:
+            x = system.solve(weight, in_TSE, rhs, x0=x0, **opts)
+        except NativeError as e:
+            if opts['precond'] != 4:
+                raise
+            # the multigrid set-up can fail for these weights (e.g. a coarsest level that is not
+            # positive definite): the block-Jacobi solve still reaches the same solution
+            print(f'smooth_fit: multigrid preconditioner unavailable ({e}); block-Jacobi for the rest of '
+                  f'the fit', flush=True)
+            system._mg = False
+            x = system.solve(weight, in_TSE, rhs, x0=x0,
+                             **_solve_opts(args, system.keep_cols.size, system.has_blocks, False))
         if system.stats['istop'] == 7:
             print(f"smooth_fit: LSQR reached its iteration limit ({system.stats['iters']}) before the "
                   f"requested tolerance; raise lsq_maxit or use lsq_precond=2", flush=True)
@@ -324,7 +337,6 @@ def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args,
     n_cols = G_data.col_N
     sums = None
     if system is not None and getattr(system, 'formation', None) == 'stencil':
-        from ._native import NativeError
         fs = {'count': tse_b.astype(float)}
         for key, vals in (('scaled', r_scaled ** 2), ('plain', r ** 2)):
             f = np.zeros(tse_b.size)

@@ -14,7 +14,7 @@ import ctypes
 import numpy as np
 import scipy.sparse as sp
 
-from ._native import LsqStats, NativeError, as_c, default_opts, load, ptr
+from ._native import LsqStats, NativeError, NativeRefused, as_c, default_opts, load, ptr
 
 
 class LSQSolver:
@@ -48,7 +48,8 @@ class LSQSolver:
 
     def _check(self, rc, what):
         if rc < 0:
-            raise NativeError(f'{what}: {self._L.lsq_last_error(self._h).decode()}')
+            cls = NativeRefused if rc == -5 else NativeError
+            raise cls(f'{what}: {self._L.lsq_last_error(self._h).decode()}')
         return rc
 
     # ---- formation ---------------------------------------------------------------------------

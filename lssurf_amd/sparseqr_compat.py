@@ -13,10 +13,12 @@ Cuthill-McKee order, else column scaling (precond 1) when the band does not fit.
 anisotropic notebook system needs > 5·10⁴ column-scaled LSQR iterations; with the band factor a
 handful.
 """
+import warnings
+
 import numpy as np
 import scipy.sparse as sp
 
-from ._native import NativeError
+from ._native import NativeRefused
 from .solver import LSQSolver
 
 _DEFAULTS = dict(atol=1e-12, btol=1e-12, conlim=1e12, precond='auto')
@@ -72,10 +74,12 @@ def solve(A, b, tolerance=None, device=0, **opts):
                 s.set_band_order(perm)
         try:
             x, stats = s.solve(b, **kw)
-        except NativeError:
+        except NativeRefused as e:       # only a declined band (memory / width); errors propagate
             if not (auto and kw['precond'] == 5):
                 raise
-            kw['precond'] = 1            # the band did not fit the device: column scaling
+            warnings.warn(f'sparseqr_compat.solve: {e}; falling back to column-scaled LSQR (slow on '
+                          'ill-conditioned systems)', RuntimeWarning)
+            kw['precond'] = 1
             x, stats = s.solve(b, **kw)
     solve.last_stats = stats
     return x

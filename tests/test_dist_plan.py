@@ -198,3 +198,27 @@ def test_slab_configs_are_one_rank_window_of_c4(name, nranks):
     assert ny == n // nranks + 2 * halo
     D, _ = synthetic.points(name)
     assert D.size == pts and np.all(np.abs(D.y) <= kw['W']['y'] / 2) and np.all(np.abs(D.x) <= kw['W']['x'] / 2)
+
+
+def test_window_problem_slices_field_values():
+    """Field-valued parts (the anisotropic directional operator) over y-slab windows: every
+    rank keeps the rows of its owned centres and exactly their field values; the ranks' rows
+    tile the global rows once."""
+    from lssurf_amd import assemble, dist, synthetic
+    S, kw = synthetic.aniso_system('ta64')
+    d = assemble.describe(S['G_data'], S['Gc'], with_fields=True)
+    stencils, npts, fields = d[3], d[4], d[5]
+    (k, off, val, fsel, F), = fields
+    s = stencils[k]
+    part = dist.SlabPartition(S['grids']['dz'], 3)
+    seen = []
+    for r in range(3):
+        prob = dist.window_problem(S['G_data'], S['Gc'], part, r, S['keep'])
+        seen.append(prob['rows'])
+        (kl, offl, vall, fsell, Fl), = prob['fields']
+        t = prob['stencils'][kl]
+        rows = prob['rows'][t.row0:t.row0 + t.n_eq] - int(s.row0)     # the part's global row indices
+        assert np.array_equal(offl, off) and np.array_equal(Fl, F[:, rows])
+        assert prob['halo'] >= 1
+    allrows = np.sort(np.concatenate(seen))
+    assert np.array_equal(allrows, np.arange(S['w'].size))

@@ -114,3 +114,45 @@ def test_device_rde_bit_identical(gpu_available, n):
             assert d(s) == RDE(r[mask] / np.sqrt(s ** 2 + sigma[mask] ** 2))
     finally:
         d.close()
+
+
+@pytest.mark.parametrize('name', ['sf3d', 'avg'])
+def test_parse_model_device_path_equals_host_path(gpu_available, name):
+    """parse_model's device reductions (constraint R / RMS by lsq_rows_sumsq, count / misfit maps
+    by lsq_data_colsum) equal its host path (the reference's products, smooth_fit.py:318-347) on
+    the same solution, to rounding."""
+    from lssurf_amd.constraint_functions import reference_epoch_keep_cols
+    from lssurf_amd.smooth_fit import DEFAULTS, FitSystem, parse_model
+    g = golden(f'sys_{name}.npz')
+    kw = golden_kwargs(g)
+    args = dict(DEFAULTS, **kw)
+    S = LS.smooth_fit(data=golden_points(g), return_fit_objects=True, **kw)
+    data, G_data, Gc, grids = S['data'], S['G_data'], S['Gc'], S['grids']
+    keep = reference_epoch_keep_cols(G_data.col_N, grids['dz'], kw['reference_epoch'])
+    rng = np.random.default_rng(4)
+    m0 = np.zeros(G_data.col_N)
+    m0[keep] = rng.standard_normal(keep.size)
+    tse = rng.random(data.size) > 0.1
+    data.assign({'three_sigma_edit': tse, 'sigma_extra': np.zeros(data.size),
+                 'z_est': G_data.toCSR().dot(m0)})
+    out = {}
+    fs = FitSystem(G_data, Gc, keep, Gc.col_N, grids=grids)
+    try:
+        fs.solver.set_row_weight(1. / np.concatenate((S['Ed'], S['Ec'])))
+        for label, system in (('host', None), ('device', fs)):
+            m, R, RMS = {}, {}, {}
+            parse_model(m, m0, data, R, RMS, G_data, {}, Gc, S['Ec'], grids, args, system=system)
+            out[label] = (m, R, RMS)
+    finally:
+        fs.close()
+    (mh, Rh, RMSh), (md, Rd, RMSd) = out['host'], out['device']
+    assert set(Rh) == set(Rd) and Rh
+    for k in Rh:
+        assert abs(Rd[k] - Rh[k]) <= 1e-12 * abs(Rh[k]), k
+        assert abs(RMSd[k] - RMSh[k]) <= 1e-12 * abs(RMSh[k]), k
+    for ff in ('z0', 'dz'):
+        for f in ('count', 'misfit_rms', 'misfit_scaled_rms'):
+            a, b = getattr(md[ff], f), getattr(mh[ff], f)
+            np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+            ok = np.isfinite(b)
+            np.testing.assert_allclose(a[ok], b[ok], rtol=1e-12, atol=0)
