@@ -216,6 +216,16 @@ int lsq_set_band_order(lsq_handle* h, int64_t n, const int32_t* perm);
 int lsq_cov_band(lsq_handle* h, const int32_t* perm, double* E, int64_t n_ops, const int64_t* op_ptr,
                  const int32_t* op_col, const double* op_val, double* op_err, int64_t* info);
 
+/* The banded factor itself (replaces sparseqr.rz's R and E, smooth_fit.py:218 / the aniso notebook):
+ * for the current weighted, masked A and the column order perm (nullable = natural),
+ * (A·P)ᵀ(A·P) = RᵀR with R = R̃·S⁻¹, R̃ the upper band factor of the equilibrated S·Pᵀ(AᵀA)P·S.
+ * info (3): n, T = tile rows (n padded to 64·T), w = tiles right of the diagonal per tile row.  When
+ * R is non-null: R̃ as T·(w+1) row-major 64×64 tiles, tile (I, J) (I ≤ J ≤ I + w) at
+ * (I·(w+1) + J − I)·4096 (use the upper triangle of diagonal tiles), sc = diag(S) (64·T), perm_out =
+ * P (new position -> compact column, n).  Call once with R = NULL for the sizes.  -5 when the band
+ * does not fit the device. */
+int lsq_band_factor(lsq_handle* h, const int32_t* perm, int64_t* info, double* R, double* sc, int32_t* perm_out);
+
 /* ---- multi-GPU (one process per GPU) --------------------------------------
  * lsq_dist_unique_id: rank 0 creates the 128-byte RCCL id; the caller broadcasts it (any
  * transport); every rank then calls lsq_create_dist.  Each rank forms only the rows it owns

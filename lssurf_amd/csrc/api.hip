@@ -594,6 +594,16 @@ int lsq_cov_band(lsq_handle* h, const int32_t* perm, double* E, int64_t n_ops, c
     });
 }
 
+int lsq_band_factor(lsq_handle* h, const int32_t* perm, int64_t* info, double* R, double* sc, int32_t* perm_out) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_band_factor: no matrix");
+        if (S.dist) return fail(S, "lsq_band_factor: not available on distributed handles");
+        if (!info) return fail(S, "lsq_band_factor: null info");
+        lsq::band_factor_download(S, perm, info, R, sc, perm_out);
+        return 0;
+    });
+}
+
 int lsq_get_rinv(lsq_handle* h, double* Rinv) {
     return guarded(h, [&](lsq::System& S) {
         if (!S.G.rp.p) return fail(S, "lsq_get_rinv: no matrix");

@@ -915,6 +915,24 @@ void band_launch_warm(System& S, const double* x0, double* y0) {
                        F.perm.p, y0);
 }
 
+// sparseqr.rz drop-in (lsq_band_factor): the band factor of the current weighted, masked system in
+// the order h_perm, downloaded (info = n, T, w; R_out: T·(w+1) row-major 64×64 tiles, tile (I, J)
+// at (I·(w+1) + J − I)·4096, upper triangle of the diagonal tiles; sc_out: S (T·64); perm_out: n).
+// Null outputs: info only.
+void band_factor_download(System& S, const int32_t* h_perm, int64_t* info, double* R_out, double* sc_out,
+                          int32_t* perm_out) {
+    refresh_scaling(S, S.cs_mode < 0 ? 0 : S.cs_mode);
+    BandFactor F;
+    band_factor(S, h_perm, F);
+    info[0] = F.n;
+    info[1] = F.T;
+    info[2] = F.w;
+    if (R_out) F.R.download(R_out, F.T * (int64_t)(F.w + 1) * TT, S.stream);
+    if (sc_out) F.sc.download(sc_out, F.T * TB, S.stream);
+    if (perm_out) F.perm.download(perm_out, F.n, S.stream);
+    HIP_CHECK(hipStreamSynchronize(S.stream));
+}
+
 void band_cov(System& S, const int32_t* h_perm, double* h_E, int64_t nops, const int64_t* h_rp, const int32_t* h_ci,
               const double* h_v, double* h_oe, int64_t* info) {
     hipStream_t st = S.stream;

@@ -418,6 +418,8 @@ void band_launch_bsub(System& S, const double* v, int scale_mode, double* out);
 void band_launch_fsub(System& S, const double* t, const double* vin, double* vout, double* part);
 void band_launch_warm(System& S, const double* x0, double* y0);
 void band_check(System& S);   // throws when a precond-5 solve's grid barrier timed out
+void band_factor_download(System& S, const int32_t* perm, int64_t* info, double* R_out, double* sc_out,
+                          int32_t* perm_out);   // sparseqr.rz drop-in (lsq_band_factor)
 void band_cov(System& S, const int32_t* perm, double* E, int64_t nops, const int64_t* rp, const int32_t* ci,
               const double* v, double* op_err, int64_t* info);   // rs/cs -> SELL values (single GPU)
 void scaling_rows_colnorm(System& S, int precond, bool raw);

@@ -239,6 +239,37 @@ class LSQSolver:
         self._check(self._L.lsq_set_band_order(self._h, n, ptr(pp) if pp is not None else None),
                     'lsq_set_band_order')
 
+    def band_factor(self, perm=None):
+        """(R, perm): (A·P)ᵀ(A·P) = RᵀR for the current weighted, masked A, R upper triangular
+        (scipy CSR, n × n, explicit zeros of the band dropped), P = perm (new position -> compact
+        column) — the R and E of sparseqr.rz (lsq_band_factor)."""
+        pp = None if perm is None else as_c(perm, np.int32)
+        info = np.zeros(3, np.int64)
+        self._check(self._L.lsq_band_factor(self._h, ptr(pp) if pp is not None else None, ptr(info), None, None, None),
+                    'lsq_band_factor')
+        n, T, w = (int(v) for v in info)
+        R = np.zeros(T * (w + 1) * 4096)
+        sc = np.zeros(T * 64)
+        po = np.zeros(n, np.int32)
+        self._check(self._L.lsq_band_factor(self._h, ptr(pp) if pp is not None else None, ptr(info), ptr(R), ptr(sc),
+                                            ptr(po)), 'lsq_band_factor')
+        tiles = R.reshape(T, w + 1, 64, 64)
+        rows, cols, vals = [], [], []
+        r64, c64 = np.meshgrid(np.arange(64), np.arange(64), indexing='ij')
+        for I in range(T):
+            for k in range(min(w + 1, T - I)):
+                t = tiles[I, k]
+                sel = (t != 0) & ((r64 <= c64) if k == 0 else True)
+                rows.append(64 * I + r64[sel])
+                cols.append(64 * (I + k) + c64[sel])
+                vals.append(t[sel])
+        rows, cols, vals = np.concatenate(rows), np.concatenate(cols), np.concatenate(vals)
+        keep = (rows < n) & (cols < n)
+        vals = vals[keep] / sc[cols[keep]]            # R = R̃ S⁻¹ (column j scaled by 1/s_j)
+        Rm = sp.csr_matrix((vals, (rows[keep], cols[keep])), shape=(n, n))
+        Rm.sort_indices()
+        return Rm, po
+
     def cov_band(self, perm=None, op=None):
         """(E, op_err, info) of the current weighted, masked system without a dense factor:
         E = sqrt(diag((AᵀA)⁻¹)) per compact column and, for the rows of `op` (scipy sparse over

@@ -89,4 +89,23 @@ solve.last_stats = None
 
 
 def rz(A, b, tolerance=None, device=0):
-    raise NotImplementedError('sparseqr.rz: use lssurf_amd.errors (normal-equation R on the device)')
+    """Drop-in for PySPQR's ``sparseqr.rz(A, b)`` (LSsurf/smooth_fit.py:218): returns
+    (Z, R, E, rank) with A[:, E] = Q·R, R upper triangular (scipy CSR), Z = Qᵀb, rank = n.
+
+    R is the Cholesky factor of (A E)ᵀ(A E) from the device band factorization (lsq_band_factor;
+    E the band order of ``band_order``), which equals SuiteSparseQR's R up to the signs of its rows
+    (R is unique for full column rank once its diagonal is positive); Z = R⁻ᵀ(A E)ᵀb.  Everything
+    the reference computes from rz — x = E·R⁻¹Z, R⁻¹ by inv_tr_upper, the error propagation — is
+    the same.  ``tolerance`` (SPQR's rank tolerance) has no meaning here: A must have full column
+    rank (a rank-deficient A raises)."""
+    from scipy.sparse.linalg import spsolve_triangular
+    A = sp.csr_matrix(A)
+    b = np.asarray(b, dtype=np.float64)
+    perm, bw = band_order(A)
+    coo = A.tocoo()
+    with LSQSolver(device) as s:
+        s.set_matrix_coo(A.shape[0], A.shape[1], coo.row, coo.col, coo.data)
+        R, E = s.band_factor(perm)
+    AE = A[:, E]
+    Z = spsolve_triangular(R.T.tocsr(), AE.T @ b, lower=True)
+    return Z, R, E, A.shape[1]
