@@ -322,12 +322,14 @@ def main():
     solve = {}
     if not args.no_solve:
         # solve wall-time with smooth_fit's default solver for this system: CGNR + the multigrid
-        # V-cycle (precond 4) where it runs (single GPU, per-node blocks), else the timed
-        # configuration; then CGNR + block-Jacobi and LSQR + block-Jacobi for comparison
+        # V-cycle (precond 4) where it runs (per-node blocks; over ranks: window level 0 + the
+        # replicated global coarse levels), else the timed configuration; then CGNR + block-Jacobi
+        # and (one GPU) LSQR + block-Jacobi for comparison
         names = {1: 'column scaling', 3: 'block-Jacobi per (y,x) node', 4: 'multigrid V-cycle (block-Jacobi smoothing)'}
         sp = args.precond
-        if (args.solve_precond == 'auto' and meth == 1 and not isinstance(solver, _Dist) and args.precond == 3
-                and solver.cg_available(4)[0]) or args.solve_precond == '4':
+        mg_ok = (getattr(fs, 'has_global', False) and fs.has_blocks) if isinstance(solver, _Dist) \
+            else solver.cg_available(4)[0]
+        if (args.solve_precond == 'auto' and meth == 1 and args.precond == 3 and mg_ok) or args.solve_precond == '4':
             sp = 4
 
         def rec(st):
@@ -345,11 +347,11 @@ def main():
         x, sst = solver.solve(rhs, op=args.op, precond=sp, method=meth)
         solve = dict(rec(sst), solve_method=['lsqr', 'cgnr'][int(sst.get('method', 0))],
                      solve_precond=names.get(sp, sp))
+        if meth == 1 and sp == 4:
+            xb, sb = solver.solve(rhs, op=args.op, precond=3, method=1)
+            solve['solve_block_jacobi'] = rec(sb)
+            solve['solve_rel_diff_vs_block_jacobi'] = float(np.linalg.norm(x - xb) / np.linalg.norm(xb))
         if meth == 1 and not isinstance(solver, _Dist):   # distributed LSQR has no block-Jacobi
-            if sp == 4:
-                xb, sb = solver.solve(rhs, op=args.op, precond=3, method=1)
-                solve['solve_block_jacobi'] = rec(sb)
-                solve['solve_rel_diff_vs_block_jacobi'] = float(np.linalg.norm(x - xb) / np.linalg.norm(xb))
             xl, sl = solver.solve(rhs, op=args.op, precond=min(args.precond, 3), method=0)
             solve['solve_lsqr'] = rec(sl)
             solve['lsqr_iters_per_s'] = solve['solve_lsqr']['solve_iters_per_s']

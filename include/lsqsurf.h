@@ -254,6 +254,18 @@ int lsq_dist_set_halo(lsq_handle* h, int32_t n_ranges, const int64_t* own_ranges
                       const int32_t* peers, const int64_t* send_cnt, const int32_t* send_idx,
                       const int64_t* recv_cnt, const int32_t* recv_idx);
 
+/* Multigrid over ranks (precond 4, method 1): the global structure behind a structured rank's
+ * window — the global grids and stencil parts (the descriptors of lsq_set_matrix_stencil for the
+ * whole system; field-valued parts with ntpl = 0), local_of[s] = the rank's stencil index of global
+ * stencil s (-1: the rank holds none of its rows), and the window in global node rows of dim 0:
+ * window start, owned rows [own_row0, own_row1), rows of the lattice.  Level 0 of the V-cycle is
+ * each rank's window (halo exchanges around every operator application), the coarse levels are
+ * the global Galerkin levels replicated on every rank (the restricted residual summed over the
+ * ranks once per cycle, the lumped data rows once per solve). */
+int lsq_dist_set_global(lsq_handle* h, int64_t n_full, int32_t n_grids, const lsq_grid_desc* grids, int32_t n_stencil,
+                        const lsq_stencil_desc* stencils, const int32_t* local_of, int32_t win_row0, int32_t own_row0,
+                        int32_t own_row1, int32_t rows);
+
 /* Virtual ranks: the same distributed solve with every rank of the partition in THIS process
  * on one device (exchanges become device copies).  Configure each rank's handle exactly as a
  * real rank (lsq_set_col_map, lsq_set_matrix_*, lsq_dist_referenced_cols,

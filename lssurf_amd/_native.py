@@ -53,7 +53,7 @@ EXPORTS = ['lsq_default_opts', 'lsq_create', 'lsq_destroy', 'lsq_last_error', 'l
            'lsq_set_column_blocks', 'lsq_shape', 'lsq_get_csr',
            'lsq_solve', 'lsq_spmv', 'lsq_spmv_rows', 'lsq_rows_sumsq', 'lsq_data_colsum', 'lsq_iterate', 'lsq_profile_kernels', 'lsq_cg_available', 'lsq_profile_cg', 'lsq_mg_info', 'lsq_mg_apply', 'lsq_normal_apply', 'lsq_sell_info', 'lsq_sigma_x', 'lsq_cov_band', 'lsq_set_band_order', 'lsq_band_factor',
            'lsq_get_rinv', 'lsq_dist_unique_id', 'lsq_create_dist', 'lsq_dist_referenced_cols',
-           'lsq_dist_set_layout', 'lsq_dist_set_halo', 'lsq_vgroup_create', 'lsq_vgroup_rank', 'lsq_vgroup_solve', 'lsq_vgroup_iterate',
+           'lsq_dist_set_layout', 'lsq_dist_set_halo', 'lsq_dist_set_global', 'lsq_vgroup_create', 'lsq_vgroup_rank', 'lsq_vgroup_solve', 'lsq_vgroup_iterate',
            'lsq_vgroup_last_error', 'lsq_vgroup_destroy',
            'lsq_rde_create', 'lsq_rde_order_stats', 'lsq_rde_last_error', 'lsq_rde_destroy',
            'tri_upper_solve_csr', 'tri_upper_inv_csr', 'tri_upper_rowrss_csr', 'tri_last_error']
@@ -107,6 +107,7 @@ def load():
         'lsq_dist_referenced_cols': ([P, P], ctypes.c_int),
         'lsq_dist_set_layout': ([P, P, i64, i64, i32, P, P, P, P], ctypes.c_int),
         'lsq_dist_set_halo': ([P, i32, P, i32, P, P, P, P, P], ctypes.c_int),
+        'lsq_dist_set_global': ([P, i64, i32, P, i32, P, P, i32, i32, i32, i32], ctypes.c_int),
         'lsq_vgroup_create': ([i32, i32], P),
         'lsq_vgroup_rank': ([P, i32], P),
         'lsq_vgroup_solve': ([P, P, P, P, P], ctypes.c_int),

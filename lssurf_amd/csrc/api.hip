@@ -289,9 +289,9 @@ int lsq_solve(lsq_handle* h, const double* b, double* x_inout, const lsq_opts* o
         if (o->method != 0 && o->method != 1) return fail(S, "lsq_solve: method must be 0 (LSQR) or 1 (CGNR)");
         if (o->precond < 0 || o->precond > 5) return fail(S, "lsq_solve: precond must be 0 .. 5");
         if (o->precond == 5 && S.dist) return fail(S, "lsq_solve: precond 5 (band factor) is single-GPU");
-        if (o->precond == 4 && (o->method != 1 || S.dist || !lsq::cg_available(S, 4)))
-            return fail(S, "lsq_solve: precond 4 (multigrid) runs CGNR (method 1) on single-GPU structured systems: " +
-                               (S.dist ? std::string("distributed rank") : o->method != 1 ? std::string("method is not 1") : S.cg_ok ? S.mg_why : S.cg_why));
+        if (o->precond == 4 && (o->method != 1 || (!S.dist && !lsq::cg_available(S, 4))))
+            return fail(S, "lsq_solve: precond 4 (multigrid) runs CGNR (method 1) on structured systems: " +
+                               (o->method != 1 ? std::string("method is not 1") : S.cg_ok ? S.mg_why : S.cg_why));
         if (S.dist) {
             if (S.virt) return fail(S, "lsq_solve: a virtual rank solves through lsq_vgroup_solve");
             lsq::Group G;
@@ -321,9 +321,9 @@ int lsq_iterate(lsq_handle* h, const double* b, int64_t iters, const lsq_opts* o
         lsq_opts d;
         lsq_default_opts(&d);
         if (!o) o = &d;
-        if (o->precond == 4 && (o->method != 1 || S.dist || !lsq::cg_available(S, 4)))
-            return fail(S, "lsq_iterate: precond 4 (multigrid) runs CGNR (method 1) on single-GPU structured systems: " +
-                               (S.dist ? std::string("distributed rank") : o->method != 1 ? std::string("method is not 1") : S.cg_ok ? S.mg_why : S.cg_why));
+        if (o->precond == 4 && (o->method != 1 || (!S.dist && !lsq::cg_available(S, 4))))
+            return fail(S, "lsq_iterate: precond 4 (multigrid) runs CGNR (method 1) on structured systems: " +
+                               (o->method != 1 ? std::string("method is not 1") : S.cg_ok ? S.mg_why : S.cg_why));
         if (S.dist) {
             if (S.virt) return fail(S, "lsq_iterate: a virtual rank iterates through lsq_vgroup_iterate");
             lsq::Group G;
@@ -480,7 +480,7 @@ int lsq_dist_set_layout(lsq_handle* h, const int32_t* col_local, int64_t n_local
         S.send_idx.upload(send_idx, ts, S.stream);
         S.sbuf.alloc(std::max<int64_t>(ts, 1));
         S.rbuf.alloc(std::max<int64_t>(ts, 1));
-        S.gsum.alloc(8);
+        S.gsum.alloc(16);
         S.gsum.zero(S.stream);
         HIP_CHECK(hipStreamSynchronize(S.stream));
         S.dist = true;
@@ -544,7 +544,7 @@ int lsq_dist_set_halo(lsq_handle* h, int32_t n_ranges, const int64_t* own_ranges
         const int64_t nb = std::max<int64_t>(std::max(ts, tr), 1);
         S.sbuf.alloc(nb);
         S.rbuf.alloc(nb);
-        S.gsum.alloc(8);
+        S.gsum.alloc(16);
         S.gsum.zero(S.stream);
         HIP_CHECK(hipStreamSynchronize(S.stream));
         S.n_own = S.G.n;
@@ -590,6 +590,34 @@ int lsq_cov_band(lsq_handle* h, const int32_t* perm, double* E, int64_t n_ops, c
         if (n_ops < 0 || (n_ops > 0 && (!op_ptr || !op_err || (op_ptr[n_ops] > 0 && (!op_col || !op_val)))))
             return fail(S, "lsq_cov_band: bad op rows");
         lsq::band_cov(S, perm, E, n_ops, op_ptr, op_col, op_val, op_err, info);
+        return 0;
+    });
+}
+
+int lsq_dist_set_global(lsq_handle* h, int64_t n_full, int32_t n_grids, const lsq_grid_desc* grids, int32_t n_stencil,
+                        const lsq_stencil_desc* stencils, const int32_t* local_of, int32_t win_row0, int32_t own_row0,
+                        int32_t own_row1, int32_t rows) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.dist_mf) return fail(S, "lsq_dist_set_global: needs a structured rank (lsq_dist_set_halo first)");
+        if (!grids || (n_stencil && (!stencils || !local_of)) || own_row0 < 0 || own_row1 <= own_row0 || win_row0 < 0 ||
+            win_row0 > own_row0 || rows < own_row1)
+            return fail(S, "lsq_dist_set_global: bad arguments");
+        lsq::describe_global(S, n_full, n_grids, grids, n_stencil, stencils);
+        S.dg_local.clear();
+        for (int s = 0; s < n_stencil; ++s) {
+            if (stencils[s].n_eq == 0) continue;
+            if (local_of[s] >= S.mfh.n_parts) return fail(S, "lsq_dist_set_global: local part out of range");
+            S.dg_local.push_back(local_of[s]);
+        }
+        S.dg_wa = win_row0;
+        S.dg_oa = own_row0;
+        S.dg_ob = own_row1;
+        S.dg_S0 = rows;
+        S.dg_on = true;
+        lsq::graph_cache_drop(&S);
+        lsq::mg_free(S.mg);
+        S.mg = nullptr;
+        S.mg_why.clear();
         return 0;
     });
 }

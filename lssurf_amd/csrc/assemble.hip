@@ -299,7 +299,51 @@ bool describe_stencil_operator(MfDesc& d, int64_t m, int64_t n_full, int32_t n_g
     return d.n_parts > 0 && covered == n_full && node0 < (int64_t(1) << 31);
 }
 
+GenSt gen_of(const lsq_stencil_desc& d) {
+    GenSt G{};
+    G.grid = d.grid;
+    G.ntpl = d.ntpl;
+    G.row0 = d.row0;
+    G.n_eq = d.n_eq;
+    for (int k = 0; k < 3; ++k) {
+        G.lo[k] = d.lo[k];
+        G.hi[k] = d.hi[k];
+    }
+    G.F = nullptr;
+    for (int t = 0; t < std::min(d.ntpl, 8); ++t) {
+        for (int k = 0; k < 3; ++k) G.off[t][k] = d.off[t][k];
+        G.val[t] = d.val[t];
+    }
+    return G;
+}
+
 }  // namespace
+
+// The global structure behind a rank's window (host only, for the distributed multigrid's coarse
+// levels): grids and stencil parts as describe_stencil_operator sees them; parts with ntpl = 0 are
+// field-valued (their coarse rows come from the ranks' partial Galerkin rows).
+void describe_global(System& S, int64_t n_full, int32_t n_grids, const lsq_grid_desc* grids, int32_t n_stencil,
+                     const lsq_stencil_desc* st) {
+    if (n_grids < 1 || n_grids > MAX_GRIDS || n_stencil < 0 || n_stencil > MAX_STENCIL)
+        throw std::invalid_argument("lsq_dist_set_global: too many grids / parts");
+    std::vector<GenSt> gs(n_stencil);
+    int64_t m = 0, npts = 0;
+    for (int s = 0; s < n_stencil; ++s) {
+        gs[s] = gen_of(st[s]);
+        if (st[s].ntpl < 0 || st[s].ntpl > 8) throw std::invalid_argument("lsq_dist_set_global: bad stencil");
+        m = std::max<int64_t>(m, st[s].row0 + st[s].n_eq);
+    }
+    MfDesc d{};
+    if (!describe_stencil_operator(d, m, n_full, n_grids, grids, npts, n_stencil, gs.data()))
+        throw std::invalid_argument("lsq_dist_set_global: the global parts are not a structured stencil operator");
+    int q = 0;
+    for (int s = 0; s < n_stencil; ++s) {   // describe_stencil_operator keeps the non-empty parts in order
+        if (st[s].n_eq == 0) continue;
+        d.p[q].var = st[s].ntpl == 0 ? 1 : 0;
+        ++q;
+    }
+    S.dg_mfh = d;
+}
 
 void form_from_stencils(System& S, int64_t m, int64_t n_full, int32_t n_grids, const lsq_grid_desc* grids,
                         int32_t n_interp, const int32_t* interp_grid, int64_t npts, const double* py,

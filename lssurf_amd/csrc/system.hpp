@@ -346,6 +346,15 @@ struct System {
     bool dist_mf = false;
     DBuf<int32_t> recv_idx;
     DBuf<uint8_t> live;
+    // distributed multigrid (lsq_dist_set_global): the global structure behind a structured rank's
+    // window — host description of the global grids and parts (row scales filled per solve), the
+    // rank's part of each global part (-1: none), global node rows of the window start and the
+    // owned rows [dg_oa, dg_ob), global node rows of the lattice
+    bool dg_on = false;
+    MfDesc dg_mfh{};
+    std::vector<int32_t> dg_local;
+    int32_t dg_wa = 0, dg_oa = 0, dg_ob = 0, dg_S0 = 0;
+    DBuf<double> dg_w;                 // scratch: the global parts' row scales (all-reduced max)
 
     // CGNR (method 1): normal-stencil description + coefficient table, rebuilt when the part
     // row scales change; vectors in the full column space
@@ -390,6 +399,7 @@ struct Group {
     std::vector<System*> ranks;
     bool virt = false;
     DBuf<double*> gs_ptrs;   // virtual all-reduce: device array of the ranks' gsum pointers
+    DBuf<double*> vec_ptrs;  // virtual vector all-reduce: the ranks' vector pointers (scratch)
 };
 
 // dist (build.hip / lsqr.hip)
@@ -405,6 +415,8 @@ void relabel_columns(System& S, const int32_t* h_map, int64_t n_local);
 void form_from_coo(System& S, int64_t m, int64_t n_full, int64_t nnz, const int64_t* r,
                    const int64_t* c, const double* v);
 void finish_formation(System& S);              // G set -> GT, SELL copies, default scaling
+void describe_global(System& S, int64_t n_full, int32_t n_grids, const lsq_grid_desc* grids, int32_t n_stencil,
+                     const lsq_stencil_desc* st);   // S.dg_mfh (lsq_dist_set_global)
 void build_dmf(System& S, int32_t n_grids, const lsq_grid_desc* grids, int32_t n_interp, const int32_t* interp_grid,
                int64_t npts, const double* py, const double* px, const double* pt);   // S.dmf (CGNR data rows)
 void ensure_sell(System& S);                    // assembled A / AT (lazy when S.mf)

@@ -157,9 +157,28 @@ def window_problem(G_data, Gc, partition, rank, keep_cols):
     keep_local = np.flatnonzero(keep_cols[pos] == l2g)
     own_ranges = [(gm['col0'] + (gm['a'] - gm['wa']) * gm['stride'], gm['col0'] + (gm['b'] - gm['wa']) * gm['stride'])
                   for gm in meta]
+    # the global description (multigrid over ranks: replicated coarse levels, lsq_dist_set_global)
+    gst, local_of, nl = [], [], 0
+    for k, s in enumerate(stencils):
+        t = type(s).from_buffer_copy(s)
+        if k in fields:
+            t.ntpl = 0                                # field-valued: its coarse rows come from the ranks
+        gst.append(t)
+        gm = meta[s.grid]
+        if max(int(s.lo[0]), gm['a']) < min(int(s.hi[0]), gm['b']):
+            local_of.append(nl)
+            nl += 1
+        else:
+            local_of.append(-1)
+    lat = {(gm['wa'], gm['a'], gm['b'], int(g.shape[0])) for gm, g in zip(meta, order)}
+    glob = None
+    if len(lat) == 1:                                 # one (y, x) lattice shared by the grids
+        wa, a, b, ny = lat.pop()
+        glob = dict(grids=list(grid_descs), stencils=gst, local_of=np.array(local_of, np.int32), wa=wa, oa=a, ob=b,
+                    rows=ny, n_full=int(max(int(g.col_0) + int(g.N_nodes) for g in order)))
     return dict(grids=grids, grid_objs=order, interp=interp, coords=coords, stencils=local, fields=local_fields,
                 npts=int(pts_own.size), rows=np.concatenate(rows), m=int(row0), n_full=int(nloc), keep=keep_local, l2g=l2g,
-                keep_global=pos[keep_local], own_ranges=own_ranges, meta=meta, halo=halo)
+                keep_global=pos[keep_local], own_ranges=own_ranges, meta=meta, halo=halo, glob=glob)
 
 
 def window_halo(grid_objs, partition, rank, halo):
@@ -215,6 +234,21 @@ def _install_halo(L, h, prob, halo):
     _HandleView(L, h).check(
         L.lsq_dist_set_halo(h, len(prob['own_ranges']), ptr(rng), peers.size, ptr(peers), ptr(send_cnt),
                             ptr(send_idx), ptr(recv_cnt), ptr(recv_idx)), 'lsq_dist_set_halo')
+
+
+def _install_global(L, h, prob):
+    """The global grids and parts + the rank's place in them (multigrid, precond 4).  A system the
+    device cannot describe globally keeps precond 1/3; precond 4 then reports why."""
+    from ._native import GridDesc, StencilDesc
+    g = prob.get('glob')
+    if g is None:
+        return False
+    ga = (GridDesc * len(g['grids']))(*g['grids'])
+    sa = (StencilDesc * max(len(g['stencils']), 1))(*g['stencils'])
+    lo = as_c(g['local_of'], np.int32)
+    rc = L.lsq_dist_set_global(h, g['n_full'], len(g['grids']), ctypes.cast(ga, ctypes.c_void_p), len(g['stencils']),
+                               ctypes.cast(sa, ctypes.c_void_p), ptr(lo), g['wa'], g['oa'], g['ob'], g['rows'])
+    return rc == 0
 
 
 def window_node_blocks(prob, keep_cols):
@@ -398,6 +432,7 @@ class DistFitSystem(_Base):
             _install_halo(self.L, self.h, self.prob,
                           window_halo(self.prob['grid_objs'], self.partition, rank, self.prob['halo']))
             self.has_blocks = _install_blocks(self.L, self.h, self.prob, keep_cols)
+            self.has_global = _install_global(self.L, self.h, self.prob)
             self.n_x = self.prob['keep'].size
         else:            # owned rows, relabelled compact columns, assembled SELL operator
             self.prob = rank_problem(G_data, Gc, self.partition, rank)
@@ -435,7 +470,8 @@ class DistFitSystem(_Base):
         _HandleView(self.L, self.h).check(self.L.lsq_set_row_weight(self.h, ptr(wl)), 'lsq_set_row_weight')
 
     def solve(self, row_weight, rhs, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, method=0):
-        """method 0: LSQR (precond 0/1); 1: CGNR (precond 1 Jacobi, 3 block-Jacobi; structured ranks)."""
+        """method 0: LSQR (precond 0/1); 1: CGNR (precond 1 Jacobi, 3 block-Jacobi, 4 multigrid; structured
+        ranks)."""
         b = self._b(row_weight, rhs)
         x = np.zeros(self.n_x)
         o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond), method=int(method))
@@ -484,6 +520,7 @@ class VirtualDistFitSystem(_Base):
                 _form_window(self.L, h, prob)
                 _install_halo(self.L, h, prob, window_halo(prob['grid_objs'], self.partition, r, prob['halo']))
                 _install_blocks(self.L, h, prob, keep_cols)
+                _install_global(self.L, h, prob)
                 self.probs.append(prob)
             self.nx = [p['keep'].size for p in self.probs]
         else:

@@ -131,13 +131,13 @@ def _single_cg(S, keep, w, rhs, precond):
     return x, st
 
 
-@pytest.mark.parametrize('precond', [3, 1])
-@pytest.mark.parametrize('nranks', [2, 3, 4])
+@pytest.mark.parametrize('precond,nranks', [(p, n) for p in (3, 1) for n in (2, 3, 4)] + [(4, n) for n in (2, 3, 4, 8)])
 def test_virtual_ranks_cgnr_match_single_gpu(gpu_available, nranks, precond):
     """Distributed CGNR (normal-stencil ranks, reverse halo of q, forward halo of z) runs the
     single-GPU recurrence with the same preconditioner (Jacobi from the global column norms;
-    block-Jacobi from the node blocks summed over the ranks), so the iteration counts agree and
-    the solutions match to the solver tolerance."""
+    block-Jacobi from the node blocks summed over the ranks; multigrid: window level 0 with halos,
+    the restriction summed over the ranks, replicated global coarse levels), so the iteration
+    counts agree and the solutions match to the solver tolerance."""
     S, kw = _t64()
     keep, w, rhs = _problem(S, kw)
     x1, st1 = _single_cg(S, keep, w, rhs, precond)
@@ -154,7 +154,7 @@ def test_virtual_ranks_cgnr_match_single_gpu(gpu_available, nranks, precond):
     assert np.linalg.norm(xd - x1) / np.linalg.norm(x1) <= 1e-8
 
 
-@pytest.mark.parametrize('precond', [3, 1])
+@pytest.mark.parametrize('precond', [3, 1, 4])
 def test_virtual_ranks_cgnr_golden_exact_solution(gpu_available, precond):
     g = golden('sys_sf3d.npz')
     kw = golden_kwargs(g)
@@ -185,3 +185,24 @@ def test_virtual_ranks_cgnr_iterate_matches_solve_prefix(gpu_available):
     assert st['method'] == 1 and st['iters'] == 20 and st2['iters'] == 20
     assert np.isclose(st['r1norm'], st2['r1norm'], rtol=1e-10)
     assert np.all(np.isfinite(x))
+
+
+def test_virtual_ranks_mg_reweight(gpu_available):
+    """Multigrid over ranks across a change of row weights and an edited row mask (the
+    editing loop): the per-solve set-up (lumped level-1 data summed over the ranks, λ by power
+    steps with halos) follows the new weights; matches the single-GPU multigrid solve."""
+    S, kw = _t64()
+    keep, w, rhs = _problem(S, kw)
+    vd = dist.VirtualDistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, 3)
+    w2 = w.copy()
+    w2[:S['data'].size:5] = 0.0        # edited data rows carry weight 0
+    w2[1:S['data'].size:7] *= 2.0
+    try:
+        vd.solve(w, rhs, atol=1e-12, btol=1e-12, conlim=1e12, precond=4, method=1)
+        xd = vd.solve(w2, rhs, atol=1e-12, btol=1e-12, conlim=1e12, precond=4, method=1)
+        std = vd.stats
+    finally:
+        vd.close()
+    x1, st1 = _single_cg(S, keep, w2, rhs, 4)
+    assert abs(std['iters'] - st1['iters']) <= 3, (std['iters'], st1['iters'])
+    assert np.linalg.norm(xd - x1) / np.linalg.norm(x1) <= 1e-8

@@ -57,11 +57,15 @@ def _rank(rank, world, port, structured, outq, opts=TOL):
 CG_TOL = dict(atol=1e-12, btol=1e-12, conlim=1e12, precond=3, method=1)
 
 
-@pytest.mark.parametrize('structured,opts', [(True, TOL), (False, TOL), (True, CG_TOL)],
-                         ids=['lsqr-structured', 'lsqr-assembled', 'cgnr-blockjacobi'])
+MG_TOL = dict(CG_TOL, precond=4)
+
+
+@pytest.mark.parametrize('structured,opts', [(True, TOL), (False, TOL), (True, CG_TOL), (True, MG_TOL)],
+                         ids=['lsqr-structured', 'lsqr-assembled', 'cgnr-blockjacobi', 'cgnr-multigrid'])
 def test_two_rccl_ranks_match_single_gpu(gpu_available, structured, opts):
     """cgnr-blockjacobi: CGNR + block-Jacobi over RCCL (halos of q and z, two all-reduces per
-    iteration, node blocks summed over the ranks before factoring)."""
+    iteration, node blocks summed over the ranks before factoring); cgnr-multigrid: the V-cycle
+    over RCCL (level-0 halos, the restricted residual all-reduced once per cycle)."""
     import torch.multiprocessing as mp
     from lssurf_amd.smooth_fit import FitSystem
     S, keep, w, rhs = _problem()
