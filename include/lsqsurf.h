@@ -280,6 +280,21 @@ int lsq_vgroup_iterate(lsq_vgroup* g, const double* const* b, int64_t iters, con
 const char* lsq_vgroup_last_error(lsq_vgroup* g);
 void lsq_vgroup_destroy(lsq_vgroup* g);
 
+/* Device group: the distributed solve over N distinct devices from ONE process (smooth_fit's
+ * n_gpus; SURVEY.md §8(b) "ranks invisible to Python").  One RCCL communicator per device
+ * (ncclCommInitAll); each solve runs every rank on its own host thread with the kernels, halos
+ * and all-reduces of a one-process-per-GPU rank.  Configure each rank's handle as a real rank
+ * (lsq_set_col_map, lsq_set_matrix_stencil, lsq_dist_set_halo, lsq_dist_set_global ...).
+ * Repeated devices are refused (NULL): one device runs the same ranks through lsq_vgroup. */
+typedef struct lsq_dgroup lsq_dgroup;
+lsq_dgroup* lsq_dgroup_create(int32_t n, const int32_t* devices);
+lsq_handle* lsq_dgroup_rank(lsq_dgroup* g, int32_t rank);
+int lsq_dgroup_solve(lsq_dgroup* g, const double* const* b, double* const* x, const lsq_opts* o, lsq_stats* s);
+int lsq_dgroup_iterate(lsq_dgroup* g, const double* const* b, int64_t iters, const lsq_opts* o,
+                       lsq_stats* s);
+const char* lsq_dgroup_last_error(lsq_dgroup* g);
+void lsq_dgroup_destroy(lsq_dgroup* g);
+
 /* ---- outlier editing (RDE.py:10-18, calc_sigma_extra.py:13-44) -----
  * calc_sigma_extra's bounded search evaluates RDE(r / sqrt(s² + σ²)) 25–30 times per outer
  * iteration.  lsq_rde_create uploads r and σ once (finite entries only); lsq_rde_order_stats

@@ -2,6 +2,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "../../include/lsqsurf.h"
@@ -777,6 +778,116 @@ int lsq_vgroup_iterate(lsq_vgroup* g, const double* const* b, int64_t iters, con
         lsq_default_opts(&d);
         const lsq_opts& oo = o ? *o : d;
         return oo.method == 1 ? lsq::group_cg_iterate(G, b, iters, oo, s) : lsq::group_iterate(G, b, iters, oo, s);
+    });
+}
+
+}  // extern "C"
+
+// ---- device group: N devices driven from one process (smooth_fit(n_gpus=N)) ------------------
+// One RCCL communicator per device (ncclCommInitAll) and, per solve, one host thread per device
+// running that rank's solve exactly as a one-process-per-GPU rank does (Group of one rank: the
+// same kernels, halos and all-reduces).  The ranks are invisible to the caller.
+struct lsq_dgroup {
+    std::vector<lsq_handle*> h;
+    std::string err;
+};
+
+extern "C" {
+
+lsq_dgroup* lsq_dgroup_create(int32_t n, const int32_t* devices) {
+    if (n < 1 || !devices) return nullptr;
+    for (int a = 0; a < n; ++a)
+        for (int b = 0; b < a; ++b)
+            if (devices[a] == devices[b]) return nullptr;   // RCCL: one rank per device (tests: lsq_vgroup)
+    auto* g = new lsq_dgroup();
+    for (int r = 0; r < n; ++r) {
+        lsq_handle* h = lsq_create(devices[r]);
+        if (!h) {
+            lsq_dgroup_destroy(g);
+            return nullptr;
+        }
+        h->sys.rank = r;
+        h->sys.nranks = n;
+        g->h.push_back(h);
+    }
+    std::vector<ncclComm_t> comms(n, nullptr);
+    std::vector<int> devs(devices, devices + n);
+    if (ncclCommInitAll(comms.data(), n, devs.data()) != ncclSuccess) {
+        lsq_dgroup_destroy(g);
+        return nullptr;
+    }
+    for (int r = 0; r < n; ++r) g->h[r]->sys.comm = comms[r];
+    return g;
+}
+
+lsq_handle* lsq_dgroup_rank(lsq_dgroup* g, int32_t rank) {
+    return (g && rank >= 0 && rank < (int)g->h.size()) ? g->h[rank] : nullptr;
+}
+
+const char* lsq_dgroup_last_error(lsq_dgroup* g) { return g ? g->err.c_str() : "null group"; }
+
+void lsq_dgroup_destroy(lsq_dgroup* g) {
+    if (!g) return;
+    for (int r = (int)g->h.size() - 1; r >= 0; --r) lsq_destroy(g->h[r]);
+    delete g;
+}
+
+}  // extern "C"
+
+// every rank's solve on its own host thread; the first failing rank's message is the group's
+template <class F>
+static int dgroup_run(lsq_dgroup* g, lsq_stats* s, F&& f) {
+    if (!g || g->h.empty()) return -1;
+    g->err.clear();
+    const int n = (int)g->h.size();
+    for (auto* h : g->h)
+        if (!h->sys.dist) {
+            g->err = "every rank of a device group needs lsq_dist_set_halo / lsq_dist_set_layout first";
+            return -2;
+        }
+    std::vector<int> rc(n, 0);
+    std::vector<lsq_stats> st(n);
+    std::vector<std::thread> th;
+    for (int r = 0; r < n; ++r)
+        th.emplace_back([&, r] {
+            std::memset(&st[r], 0, sizeof(lsq_stats));
+            rc[r] = guarded(g->h[r], [&](lsq::System& S) {
+                lsq::Group G;
+                G.ranks = {&S};
+                return f(G, r, &st[r]);
+            });
+        });
+    for (auto& t : th) t.join();
+    for (int r = 0; r < n; ++r)
+        if (rc[r] < 0) {
+            g->err = "rank " + std::to_string(r) + ": " + g->h[r]->sys.err;
+            return rc[r];
+        }
+    if (s) *s = st[0];
+    return rc[0];
+}
+
+extern "C" {
+
+int lsq_dgroup_solve(lsq_dgroup* g, const double* const* b, double* const* x, const lsq_opts* o, lsq_stats* s) {
+    if (!b || !x) return -1;
+    lsq_opts d;
+    lsq_default_opts(&d);
+    const lsq_opts& oo = o ? *o : d;
+    return dgroup_run(g, s, [&](lsq::Group& G, int r, lsq_stats* st) {
+        double* xs[1] = {x[r]};
+        return oo.method == 1 ? lsq::group_cg_solve(G, &b[r], xs, oo, st) : lsq::group_solve(G, &b[r], xs, oo, st);
+    });
+}
+
+int lsq_dgroup_iterate(lsq_dgroup* g, const double* const* b, int64_t iters, const lsq_opts* o, lsq_stats* s) {
+    if (!b) return -1;
+    lsq_opts d;
+    lsq_default_opts(&d);
+    const lsq_opts& oo = o ? *o : d;
+    return dgroup_run(g, s, [&](lsq::Group& G, int r, lsq_stats* st) {
+        return oo.method == 1 ? lsq::group_cg_iterate(G, &b[r], iters, oo, st)
+                              : lsq::group_iterate(G, &b[r], iters, oo, st);
     });
 }
 

@@ -501,32 +501,45 @@ class DistFitSystem(_Base):
 
 
 class VirtualDistFitSystem(_Base):
-    """All ranks of the partition in this process on one GPU (liblsqsurf virtual group):
-    identical kernels, plans and exchange order as the RCCL path."""
+    """All ranks of the partition in this process.  On one GPU (default; liblsqsurf virtual
+    group): identical kernels, plans and exchange order as the RCCL path, exchanges are device
+    copies.  With `devices` (distinct ids): liblsqsurf's device group, one RCCL communicator per
+    device (ncclCommInitAll) and one host thread per rank during a solve."""
 
-    def __init__(self, G_data, Gc, keep_cols, n_full, nranks, device=0, structured=True):
+    def __init__(self, G_data, Gc, keep_cols, n_full, nranks, device=0, structured=True, devices=None):
         self.L = load()
         self._setup_common(G_data, Gc, keep_cols, n_full, nranks)
         self.nranks = nranks
         self.structured = structured
-        self.g = self.L.lsq_vgroup_create(int(device), int(nranks))
+        if devices is not None:
+            devs = as_c(np.asarray(devices, np.int32), np.int32)
+            if devs.size != nranks or np.unique(devs).size != nranks:
+                raise ValueError('a device group needs one distinct device per rank')
+            self._api = 'lsq_dgroup'
+            self.g = self.L.lsq_dgroup_create(int(nranks), ptr(devs))
+        else:
+            self._api = 'lsq_vgroup'
+            self.g = self.L.lsq_vgroup_create(int(device), int(nranks))
         if not self.g:
-            raise NativeError('lsq_vgroup_create failed')
+            raise NativeError(f'{self._api}_create failed')
         self.probs = []
+        self.has_blocks = self.has_global = structured
         if structured:
             for r in range(nranks):
-                h = self.L.lsq_vgroup_rank(self.g, r)
+                h = self._rank(r)
                 prob = window_problem(G_data, Gc, self.partition, r, keep_cols)
                 _form_window(self.L, h, prob)
                 _install_halo(self.L, h, prob, window_halo(prob['grid_objs'], self.partition, r, prob['halo']))
-                _install_blocks(self.L, h, prob, keep_cols)
-                _install_global(self.L, h, prob)
+                self.has_blocks &= _install_blocks(self.L, h, prob, keep_cols)
+                self.has_global &= _install_global(self.L, h, prob)
                 self.probs.append(prob)
             self.nx = [p['keep'].size for p in self.probs]
         else:
+            if self._api == 'lsq_dgroup':
+                raise NotImplementedError('device groups run structured ranks')
             flags_all = []
             for r in range(nranks):
-                h = self.L.lsq_vgroup_rank(self.g, r)
+                h = self._rank(r)
                 prob = rank_problem(G_data, Gc, self.partition, r)
                 flags_all.append(_form_rank(self.L, h, prob, keep_cols, n_full))
                 self.probs.append(prob)
@@ -534,24 +547,47 @@ class VirtualDistFitSystem(_Base):
             self.layouts = [local_layout(flags_all[r], owner, r) for r in range(nranks)]
             ghosts_of = [lay[3] for lay in self.layouts]
             for r in range(nranks):
-                _install_layout(self.L, self.L.lsq_vgroup_rank(self.g, r), self.layouts[r],
-                                exchange_plan(r, self.layouts[r][0], ghosts_of))
+                _install_layout(self.L, self._rank(r), self.layouts[r], exchange_plan(r, self.layouts[r][0], ghosts_of))
             self.nx = [lay[2] for lay in self.layouts]
         self.stats = None
 
+    def _fn(self, name):
+        return getattr(self.L, f'{self._api}_{name}')
+
+    def _rank(self, r):
+        return self._fn('rank')(self.g, r)
+
     def _check(self, rc, what):
         if rc < 0:
-            raise NativeError(f'{what}: {self.L.lsq_vgroup_last_error(self.g).decode()}')
+            raise NativeError(f'{what}: {self._fn("last_error")(self.g).decode()}')
 
     def _bs(self, row_weight, rhs):
         if row_weight is not None:
             for r, prob in enumerate(self.probs):
-                h = self.L.lsq_vgroup_rank(self.g, r)
+                h = self._rank(r)
                 wl = as_c(np.asarray(row_weight)[prob['rows']], np.float64)
                 _HandleView(self.L, h).check(self.L.lsq_set_row_weight(h, ptr(wl)), 'lsq_set_row_weight')
         if rhs is not None:
             self._b_local = [as_c(np.asarray(rhs)[prob['rows']], np.float64) for prob in self.probs]
-        return self._b_local
+        return getattr(self, '_b_local', None)
+
+    def set_row_mask(self, keep):
+        """Rows kept in the solve (global row order; None: all)."""
+        for r, prob in enumerate(self.probs):
+            h = self._rank(r)
+            k = None if keep is None else as_c(np.asarray(keep, bool)[prob['rows']], np.uint8)
+            _HandleView(self.L, h).check(self.L.lsq_set_row_mask(h, ptr(k)), 'lsq_set_row_mask')
+
+    def data_forward(self, x, n_data):
+        """G_data · x for the global compact x (every data row on the rank that owns it)."""
+        out = np.empty(int(n_data))
+        for r, prob in enumerate(self.probs):
+            h = self._rank(r)
+            xl = as_c(np.asarray(x)[prob['keep_global']], np.float64)
+            y = np.zeros(prob['npts'])
+            _HandleView(self.L, h).check(self.L.lsq_spmv_rows(h, 0, prob['npts'], ptr(xl), ptr(y)), 'lsq_spmv_rows')
+            out[prob['rows'][:prob['npts']]] = y
+        return out
 
     def solve(self, row_weight, rhs, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, method=0):
         bs = self._bs(row_weight, rhs)
@@ -560,7 +596,7 @@ class VirtualDistFitSystem(_Base):
         xp = (ctypes.c_void_p * self.nranks)(*[x.ctypes.data for x in xs])
         o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond), method=int(method))
         st = LsqStats()
-        self._check(self.L.lsq_vgroup_solve(self.g, bp, xp, ctypes.byref(o), ctypes.byref(st)), 'lsq_vgroup_solve')
+        self._check(self._fn('solve')(self.g, bp, xp, ctypes.byref(o), ctypes.byref(st)), f'{self._api}_solve')
         self.stats = st.as_dict()
         x = np.zeros(self.keep_cols.size)
         for r, xr in enumerate(xs):
@@ -575,15 +611,75 @@ class VirtualDistFitSystem(_Base):
         bp = (ctypes.c_void_p * self.nranks)(*[b.ctypes.data for b in bs])
         o = default_opts(precond=int(precond), method=int(method))
         st = LsqStats()
-        self._check(self.L.lsq_vgroup_iterate(self.g, bp, int(iters), ctypes.byref(o), ctypes.byref(st)),
-                    'lsq_vgroup_iterate')
+        self._check(self._fn('iterate')(self.g, bp, int(iters), ctypes.byref(o), ctypes.byref(st)),
+                    f'{self._api}_iterate')
         return st.as_dict()
 
     def close(self):
         if getattr(self, 'g', None):
-            self.L.lsq_vgroup_destroy(self.g)
+            self._fn('destroy')(self.g)
             self.g = None
 
 
+class MultiDeviceFitSystem:
+    """smooth_fit's device system over several GPUs of this process (smooth_fit(n_gpus=N)): the
+    y-slab ranks of a device group (distinct devices) or, for testing on one GPU, a virtual group.
+    The FitSystem surface iterate_fit uses: solve with re-weighting and row editing, expand,
+    data_forward.  Warm starts are not used (every solve starts from x = 0)."""
+    formation = 'stencil'
+    dense_ok = False        # no single-GPU dense factor over ranks
+
+    def __init__(self, G_data, Gc, keep_cols, n_full, devices):
+        self.n_data, self.n_con = int(G_data.N_eq), int(Gc.N_eq)
+        self.keep_cols = np.asarray(keep_cols)
+        self.n_full = int(n_full)
+        devices = [int(d) for d in devices]
+        same = len(set(devices)) == 1 and len(devices) > 1
+        self.group = VirtualDistFitSystem(G_data, Gc, keep_cols, n_full, len(devices), device=devices[0],
+                                          devices=None if same else devices)
+        self.has_blocks = self.group.has_blocks
+        self._mg = None
+        self.mg_build_s = 0.0
+        self.stats = None
+        self._w_last = self._keep_last = self._rhs_last = None
+
+    def multigrid_available(self, row_weight=None):
+        """Multigrid over the ranks (precond 4) needs node blocks and the global description on
+        every rank; its levels are built by the first solve (a failure there falls back)."""
+        if self._mg is None:
+            self._mg = bool(self.group.has_blocks and self.group.has_global)
+        return self._mg
+
+    def solve(self, row_weight, data_keep, rhs, x0=None, **opts):
+        if row_weight is not self._w_last:
+            self.group._bs(row_weight, None)
+            self._w_last = row_weight
+        dk = np.asarray(data_keep, dtype=bool)
+        if self._keep_last is None or not np.array_equal(dk, self._keep_last):
+            self.group.set_row_mask(np.concatenate([dk, np.ones(self.n_con, dtype=bool)]))
+            self._keep_last = dk.copy()
+        if opts.get('precond') in (0, 2, 5):   # single-GPU factorisations: the ranks' block-Jacobi instead
+            opts = dict(opts, precond=3 if self.has_blocks else 1, method=1 if self.has_blocks else 0)
+        if rhs is self._rhs_last:
+            rhs = None                         # the ranks keep their slices
+        else:
+            self._rhs_last = rhs
+        x = self.group.solve(None, rhs, **{k: v for k, v in opts.items() if k in ('atol', 'btol', 'conlim', 'maxit',
+                                                                                    'precond', 'method')})
+        self.stats = self.group.stats
+        return x
+
+    def expand(self, x):
+        m0 = np.zeros(self.n_full)
+        m0[self.keep_cols] = x
+        return m0
+
+    def data_forward(self, x):
+        return self.group.data_forward(x, self.n_data)
+
+    def close(self):
+        self.group.close()
+
+
 __all__ = ['SlabPartition', 'rank_problem', 'column_owner', 'local_layout', 'exchange_plan', 'DistFitSystem',
-           'VirtualDistFitSystem', 'LSQSolver']
+           'VirtualDistFitSystem', 'MultiDeviceFitSystem', 'LSQSolver']

@@ -49,7 +49,7 @@ DEFAULTS = {'reference_epoch': 0, 'W_ctr': 1e4, 'return_fit_objects': False, 'ma
             # the tolerance documented in DESIGN.md §Parity)
             'device': 0, 'lsq_atol': 1e-12, 'lsq_btol': 1e-12, 'lsq_conlim': 1e12, 'lsq_maxit': 0,
             'lsq_precond': 'auto', 'lsq_dense_max': 16384, 'lsq_warm_start': True, 'lsq_method': 'auto',
-            'lsq_E_method': 'band'}
+            'lsq_E_method': 'band', 'n_gpus': 1, 'devices': None}
 
 OUT_OF_SCOPE = ('bias_params', 'sensor_grid_bias_params', 'prior_args', 'prior_edge_args', 'lagrangian_coords',
                 'constraint_scaling_maps', 'mask_file', 'bias_edit_vals')
@@ -142,14 +142,14 @@ def print_TOC(G_data, Gc):
             print(f'\t{name}: {len(np.unique(rr)) / 1000}K')
 
 
-def _solve_opts(args, n, has_blocks=False, multigrid=False):
+def _solve_opts(args, n, has_blocks=False, multigrid=False, dense_ok=True):
     """LSQR options.  precond 'auto': the exact dense-Cholesky preconditioner (R⁻¹ on the
-    device) when n <= lsq_dense_max, else the geometric multigrid V-cycle (precond 4, CGNR) when
-    the system supports it, else block-Jacobi per (y, x) node when the system has node blocks,
-    else column scaling (maxit 50 n for the iterative ones)."""
+    device) when n <= lsq_dense_max (one GPU only), else the geometric multigrid V-cycle
+    (precond 4, CGNR) when the system supports it, else block-Jacobi per (y, x) node when the
+    system has node blocks, else column scaling (maxit 50 n for the iterative ones)."""
     pc_ = args['lsq_precond']
     if pc_ == 'auto':
-        pc_ = 2 if n <= args['lsq_dense_max'] else (4 if multigrid else (3 if has_blocks else 1))
+        pc_ = 2 if dense_ok and n <= args['lsq_dense_max'] else (4 if multigrid else (3 if has_blocks else 1))
     maxit = args['lsq_maxit'] or (0 if pc_ == 2 else 50 * n)
     # method 'auto': CGNR (normal-stencil operator, column-space only) with the iterative
     # preconditioners — the library falls back to LSQR where the structured operator is absent
@@ -185,11 +185,12 @@ def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grid
         tic = time()
         m0_last = m0
         x0 = x if (args['lsq_warm_start'] and x is not None) else None
-        mg = args['lsq_precond'] == 'auto' and system.keep_cols.size > args['lsq_dense_max'] and \
+        dense_ok = getattr(system, 'dense_ok', True)
+        mg = args['lsq_precond'] == 'auto' and (system.keep_cols.size > args['lsq_dense_max'] or not dense_ok) and \
             system.multigrid_available(weight)
         if mg and 'mg_build' not in timing:
             timing['mg_build'] = system.mg_build_s
-        opts = _solve_opts(args, system.keep_cols.size, system.has_blocks, mg)
+        opts = _solve_opts(args, system.keep_cols.size, system.has_blocks, mg, dense_ok)
         try:
             x = system.solve(weight, in_TSE, rhs, x0=x0, **opts)
         except NativeError as e:
@@ -201,7 +202,7 @@ def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grid
                   f'the fit', flush=True)
             system._mg = False
             x = system.solve(weight, in_TSE, rhs, x0=x0,
-                             **_solve_opts(args, system.keep_cols.size, system.has_blocks, False))
+                             **_solve_opts(args, system.keep_cols.size, system.has_blocks, False, dense_ok))
         if system.stats['istop'] == 7:
             print(f"smooth_fit: LSQR reached its iteration limit ({system.stats['iters']}) before the "
                   f"requested tolerance; raise lsq_maxit or use lsq_precond=2", flush=True)
@@ -449,7 +450,13 @@ def smooth_fit(**kwargs):
     try:
         if args['max_iterations'] > 0:
             tic = time()
-            system = FitSystem(G_data, Gc, keep_cols, Gc.col_N, device=args['device'], grids=grids)
+            devices = args['devices'] if args['devices'] is not None else \
+                [args['device'] + k for k in range(int(args['n_gpus']))]
+            if len(devices) > 1:   # y-slab ranks on several devices of this process (lssurf_amd.dist)
+                from .dist import MultiDeviceFitSystem
+                system = MultiDeviceFitSystem(G_data, Gc, keep_cols, Gc.col_N, devices)
+            else:
+                system = FitSystem(G_data, Gc, keep_cols, Gc.col_N, device=devices[0], grids=grids)
             timing['device_setup'] = time() - tic
             tic_iteration = time()
             m0, sigma_extra, in_TSE, rs_data = iterate_fit(data, system, rhs, 1. / TCinv_diag, G_data, Gc, in_TSE,
@@ -467,7 +474,8 @@ def smooth_fit(**kwargs):
             averaging_ops = setup_averaging_ops(grids['dz'], grids['dz'].col_N, args, grids['dz'].cell_area)
             averaging_ops.update(setup_z0_avg(grids, grids['dz'].col_N, args))
             averaging_ops.update(setup_avg_mask_ops(grids['dz'], G_data.col_N, args['avg_masks'], args['dzdt_lags']))
-            parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args, system=system)
+            parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args,
+                        system=system if isinstance(system, FitSystem) else None)
             tse = data.three_sigma_edit == 1
             r_data = data.z_est[tse] - data.z[tse]
             R['data'] = np.sum((r_data / data.sigma[tse]) ** 2)
