@@ -461,6 +461,75 @@ void form_from_stencils(System& S, int64_t m, int64_t n_full, int32_t n_grids, c
     if (S.mf) build_dmf(S, n_grids, grids, n_interp, interp_grid, npts, py, px, pt);
 }
 
+// z0 (gz) on a 2× refinement of the dz (g3) lattice: the points sorted by dz cell with their dz
+// subscripts — the data rows of the system Galerkin-projected onto the dz lattice (z0's bilinear
+// interpolation composed with the bilinear prolongation is the dz-lattice interpolation), the
+// multigrid's level 1 (mg.inc mg_build_mixed).  Held by S.mx (column layout: z0 then dz).
+void build_dmf_mixed(System& S, const lsq_grid_desc& gz, const lsq_grid_desc& g3, int64_t npts, const double* py,
+                     const double* px, const double* pt) {
+    DmfDesc D{};
+    D.S0 = (int32_t)g3.shape[0];
+    D.S1 = (int32_t)g3.shape[1];
+    D.S2 = (int32_t)g3.shape[2];
+    if (D.S0 < 2 || D.S1 < 2 || (int64_t)D.S0 * D.S1 * (1 + D.S2) >= (int64_t(1) << 31)) return;
+    D.n2 = 1;
+    D.col2[0] = 0;
+    D.n3 = 1;
+    D.col3 = (int64_t)D.S0 * D.S1;
+    D.npts = npts;
+    const int64_t C1 = D.S1 - 1, ncell = (int64_t)(D.S0 - 1) * C1;
+    auto cell = [](double f, int S) {
+        const int c = (int)std::floor(f);
+        return std::min(std::max(c, 0), S - 2);
+    };
+    std::vector<double> F(3 * npts);
+    std::vector<int64_t> key(npts);
+    std::vector<int32_t> cnt(ncell + 1, 0);
+    for (int64_t r = 0; r < npts; ++r) {
+        const double fy = (py[r] - g3.b0[0]) / g3.delta[0], fx = (px[r] - g3.b0[1]) / g3.delta[1];
+        const double ft = (pt[r] - g3.b0[2]) / g3.delta[2];
+        if (!(fy >= 0.0 && fy <= D.S0 - 1 && fx >= 0.0 && fx <= D.S1 - 1 && ft >= 0.0 && ft <= D.S2 - 1)) return;
+        F[3 * r] = fy;
+        F[3 * r + 1] = fx;
+        F[3 * r + 2] = ft;
+        key[r] = (int64_t)cell(fy, D.S0) * C1 + cell(fx, D.S1);
+        ++cnt[key[r] + 1];
+    }
+    for (int64_t c = 0; c < ncell; ++c) cnt[c + 1] += cnt[c];
+    std::vector<int32_t> perm(npts), slot(cnt.begin(), cnt.end() - 1);
+    std::vector<double> P(4 * npts);
+    for (int64_t r = 0; r < npts; ++r) {
+        const int32_t i = slot[key[r]]++;
+        perm[i] = (int32_t)r;
+        P[4 * i] = F[3 * r];
+        P[4 * i + 1] = F[3 * r + 1];
+        P[4 * i + 2] = F[3 * r + 2];
+        P[4 * i + 3] = 1.0;
+    }
+    auto* X = new System();
+    X->device = S.device;
+    X->stream = S.stream;
+    X->own_stream = false;
+    X->dmf_pt.alloc(4 * npts);
+    X->dmf_pt.upload(P.data(), 4 * npts, S.stream);
+    X->dmf_perm.alloc(npts);
+    X->dmf_perm.upload(perm.data(), npts, S.stream);
+    X->dmf_cell.alloc(ncell + 1);
+    X->dmf_cell.upload(cnt.data(), ncell + 1, S.stream);
+    HIP_CHECK(hipStreamSynchronize(S.stream));
+    D.ok = 1;
+    X->dmf = D;
+    X->mfh.npts = npts;
+    S.mx = X;
+    S.mx_z0col = (int32_t)gz.col0;
+    S.mx_dzcol = (int32_t)g3.col0;
+    S.mx_Sf0 = (int32_t)gz.shape[0];
+    S.mx_Sf1 = (int32_t)gz.shape[1];
+    S.mx_Sc0 = D.S0;
+    S.mx_Sc1 = D.S1;
+    S.mx_nt = D.S2;
+}
+
 // Matrix-free CGNR data rows (DmfDesc): eligible when every interpolation grid is 2-D or 3-D on one
 // shared (y, x) lattice (≤ 2 2-D parts, ≤ 1 3-D part with ≤ CG_MAXT t nodes).  The float
 // subscripts are computed here exactly as k_gen_rows computes them (one IEEE division each), the
@@ -468,17 +537,20 @@ void form_from_stencils(System& S, int64_t m, int64_t n_full, int32_t n_grids, c
 void build_dmf(System& S, int32_t n_grids, const lsq_grid_desc* grids, int32_t n_interp, const int32_t* interp_grid,
                int64_t npts, const double* py, const double* px, const double* pt) {
     S.dmf = DmfDesc{};
+    delete S.mx;
+    S.mx = nullptr;
     if (const char* e = getenv("LSQ_CG_DMF"))
         if (e[0] == '0') return;
     if (n_interp < 1 || npts < 1 || npts >= (int64_t(1) << 31)) return;
     const lsq_grid_desc& g0 = grids[interp_grid[0]];
     DmfDesc D{};
     const lsq_grid_desc* g3 = nullptr;
+    bool shared = true;
     for (int k = 0; k < n_interp; ++k) {
         const lsq_grid_desc& g = grids[interp_grid[k]];
         if (g.ndim < 2 || g.ndim > 3) return;
         for (int d = 0; d < 2; ++d)
-            if (g.shape[d] != g0.shape[d] || g.b0[d] != g0.b0[d] || g.delta[d] != g0.delta[d]) return;
+            if (g.shape[d] != g0.shape[d] || g.b0[d] != g0.b0[d] || g.delta[d] != g0.delta[d]) shared = false;
         if (g.ndim == 2) {
             if (D.n2 == 2) return;
             D.col2[D.n2++] = g.col0;
@@ -488,6 +560,14 @@ void build_dmf(System& S, int32_t n_grids, const lsq_grid_desc* grids, int32_t n
             D.n3 = 1;
             g3 = &g;
         }
+    }
+    if (!shared) {   // z0 on a 2× refinement of the dz lattice: the multigrid's coarse data rows
+        if (n_interp != 2 || D.n2 != 1 || D.n3 != 1) return;
+        const lsq_grid_desc& gz = grids[interp_grid[0]].ndim == 2 ? grids[interp_grid[0]] : grids[interp_grid[1]];
+        for (int d = 0; d < 2; ++d)
+            if (gz.shape[d] != 2 * g3->shape[d] - 1 || gz.b0[d] != g3->b0[d] || 2.0 * gz.delta[d] != g3->delta[d]) return;
+        build_dmf_mixed(S, gz, *g3, npts, py, px, pt);
+        return;
     }
     if (g0.shape[0] < 2 || g0.shape[1] < 2 || (int64_t)g0.shape[0] * g0.shape[1] >= (int64_t(1) << 31)) return;
     D.S0 = (int32_t)g0.shape[0];

@@ -856,6 +856,7 @@ void relabel_columns(System& S, const int32_t* h_map, int64_t n_local) {
 
 System::~System() {
     mg_free(mg);
+    delete mx;
     if (comm) (void)ncclCommDestroy(comm);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);

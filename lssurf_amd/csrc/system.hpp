@@ -371,6 +371,12 @@ struct System {
     std::vector<CgVar> cg_var;       // field-valued parts (k_cg_var2d), partial slots after the x-edge pass
     int cg_nvb = 0;                  // their workgroups (partial slots)
     MgHier* mg = nullptr;            // precond 4: geometric multigrid levels (mg.inc), built lazily
+    // z0 on a 2× refinement of the dz (y, x) lattice (the reference notebooks' z0 50 m / dz 100 m):
+    // the multigrid's level 1 is the system Galerkin-projected onto the dz lattice (z0 restricted
+    // bilinearly, dz unchanged) — a shared-lattice system with matrix-free data rows (the points
+    // sorted by dz cell, z0 interpolated on the dz lattice), held here; mg.inc builds the rest
+    System* mx = nullptr;
+    int32_t mx_z0col = 0, mx_dzcol = 0, mx_Sf0 = 0, mx_Sf1 = 0, mx_Sc0 = 0, mx_Sc1 = 0, mx_nt = 0;
     std::string mg_why;              // why precond 4 is unavailable
     std::vector<double> cg_wkey;   // part row scales the table was built for
     DBuf<double> cg_x, cg_s, cg_z, cg_p0, cg_p1, cg_q, cg_t, cg_part_g, cg_part_r, cg_part_t;

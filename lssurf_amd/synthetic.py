@@ -1,6 +1,6 @@
 """Synthetic point clouds for the BASELINE.json configurations.
 
-Domain W_x = W_y = (n-1)*100 m centred on 0, spacing z0 = dz = 100 m, dt = 0.25,
+Domain W_x = W_y = (n-1)*100 m centred on 0, spacing z0 = dz = 100 m (Z0_REFINED: z0 50 m), dt = 0.25,
 W_t = (nt-1)*0.25, reference_epoch = nt//2; points uniform in (x, y, t) from
 default_rng(20251121 + config_id); z = 10 sin(2πx/Lx) cos(2πy/Ly) + 0.5 t exp(-r²/(W/4)²)
 + N(0, 0.1), Lx = W/2, Ly = W/3, sigma = 0.1; E_RMS = notebook cell-17 set.
@@ -32,15 +32,21 @@ CONFIGS = {
     'c5a': (2048, 12, 8_000_000),
     'ta64': (64, 12, 8_192),
     'ta100': (100, 8, 20_000),     # two dim-1 tiles of k_cg_var2d, 13 tile rows
+    # z0 on a 2× refinement of the dz lattice (spacing z0 50 m, dz 100 m: the reference notebooks'
+    # setup): n dz nodes per side, 2n − 1 z0 nodes
+    't64z': (64, 12, 8_192),
+    'c3z': (512, 12, 1_000_000),
 }
 ANISO = ('c5a', 'ta64', 'ta100')
+Z0_REFINED = ('t64z', 'c3z')
 
 
 def config_kwargs(name, stiff=False):
     n, nt, npts = CONFIGS[name][:3]
     ny = CONFIGS[name][3] if len(CONFIGS[name]) > 3 else n   # node rows (y) when not square
     W = {'x': (n - 1) * 100., 'y': (ny - 1) * 100., 't': (nt - 1) * 0.25}
-    return dict(W=W, ctr={'x': 0., 'y': 0., 't': 0.}, spacing={'z0': 100., 'dz': 100., 'dt': 0.25},
+    z0s = 50. if name in Z0_REFINED else 100.
+    return dict(W=W, ctr={'x': 0., 'y': 0., 't': 0.}, spacing={'z0': z0s, 'dz': 100., 'dt': 0.25},
                 E_RMS=dict(E_RMS_STIFF if stiff else E_RMS_NOTEBOOK), reference_epoch=nt // 2), npts
 
 

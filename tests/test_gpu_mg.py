@@ -72,13 +72,14 @@ def test_mg_vcycle_is_spd(gpu_available):
     assert u @ Vu > 0 and v @ Vv > 0
 
 
-@pytest.mark.parametrize('name', ['sf3d', 'sf3d_edit', 'nb_xt'])
+@pytest.mark.parametrize('name', ['sf3d', 'sf3d_edit', 'nb_xt', 'nb_err'])
 def test_mg_pcg_matches_exact_solution(gpu_available, name):
+    """sf3d: z0 and dz on one lattice; sf3d_edit / nb_xt / nb_err: z0 on a 2× refinement of the dz
+    lattice (the notebooks' z0 50 m / dz 100 m) — the hierarchy starts with the z0-refined level."""
     g, fs, w, rhs = _golden_system(name)
     try:
         ok, why = fs.solver.cg_available(4)
-        if not ok:
-            pytest.skip(f'multigrid unavailable on {name}: {why}')
+        assert ok, why
         x = fs.solve(w, np.ones(fs.n_data, bool), rhs, precond=4, method=1, maxit=5000, **TOL)
         st = fs.stats
     finally:
@@ -152,3 +153,62 @@ def test_smooth_fit_multigrid_default(gpu_available):
         assert np.linalg.norm(got[ok] - ref[ok]) / np.linalg.norm(ref[ok]) < 1e-6
     assert np.nanmax(np.abs(out['m']['dz'].dz - g['dz'])) < ABS
     assert np.array_equal(out['data'].three_sigma_edit, g['data_three_sigma_edit'])
+
+
+def _mixed_system(which):
+    if which == 't64z':
+        S, fs, w, rhs = _synthetic_system('t64z')
+    else:
+        g, fs, w, rhs = _golden_system(which)
+    return fs, w, rhs
+
+
+@pytest.mark.parametrize('which', ['t64z', 'nb_xt', 'sf3d_edit'])
+def test_mg_z0_refined_operator_and_vcycle(gpu_available, which):
+    """z0 on a 2× refinement of the dz lattice: the fine level's operator equals AᵀA of the formed
+    A (≤ 1e-12), the hierarchy below is the dz lattice's (level 1: the dz lattice), and the
+    V-cycle is symmetric positive definite."""
+    fs, w, rhs = _mixed_system(which)
+    rng = np.random.default_rng(9)
+    keep = rng.random(fs.n_data) > 0.1
+    try:
+        _prepare(fs, w, keep)
+        levels, tref = fs.solver.mg_info()
+        assert levels[0][2] == fs.n_full and levels[1][0] == (levels[0][0] + 1) // 2
+        A = fs.solver.get_csr()
+        nf = fs.n_full
+        kmask = np.zeros(nf, bool)
+        kmask[fs.keep_cols] = True
+        x = np.where(kmask, rng.standard_normal(nf), 0.0)
+        y = fs.solver.mg_apply(0, 0, x)[fs.keep_cols]
+        yr = A.T @ (A @ x[fs.keep_cols])
+        assert np.abs(y - yr).max() <= 1e-12 * np.abs(yr).max()
+        assert fs.solver.mg_apply(0, 2) > 0.5
+        u = np.where(kmask, rng.standard_normal(nf), 0.0)
+        v = np.where(kmask, rng.standard_normal(nf), 0.0)
+        Vu, Vv = fs.solver.mg_apply(0, 1, u), fs.solver.mg_apply(0, 1, v)
+    finally:
+        fs.close()
+    assert np.all(Vu[~kmask] == 0.0)
+    a, b = v @ Vu, u @ Vv
+    assert abs(a - b) <= 1e-10 * (abs(a) + abs(b)), (a, b)
+    assert u @ Vu > 0 and v @ Vv > 0
+
+
+def test_mg_z0_refined_iterations(gpu_available):
+    """t64z (z0 127², dz 64² × 12): multigrid and block-Jacobi CGNR reach the same solution, the
+    V-cycle in a fraction of the iterations; edited rows and re-weighting included."""
+    fs, w, rhs = _mixed_system('t64z')
+    rng = np.random.default_rng(4)
+    keep = rng.random(fs.n_data) > 0.1
+    w2 = w * np.where(np.arange(w.size) < fs.n_data, rng.uniform(0.5, 2, w.size), 1.0)
+    try:
+        xb = fs.solve(w2, keep, rhs, precond=3, method=1, **TOL)
+        it_bj = fs.stats['iters']
+        xm = fs.solve(w2, keep, rhs, precond=4, method=1, **TOL)
+        st = dict(fs.stats)
+    finally:
+        fs.close()
+    assert st['method'] == 1 and st['istop'] in (1, 2), st
+    assert np.linalg.norm(xm - xb) / np.linalg.norm(xb) <= 1e-8
+    assert st['iters'] * 4 <= it_bj, (st['iters'], it_bj)

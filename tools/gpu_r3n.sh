@@ -1,0 +1,7 @@
+set -uo pipefail
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r3n}
+mkdir -p $OUT
+cd $GRAFT_REPO_ROOT
+timeout -k 10 200 python -u tools/mgx_debug2.py sf3d sf3d_edit 2>&1 | tail -6
+timeout -k 10 400 python -u -m pytest tests/test_gpu_mg.py tests/test_gpu_cgnr.py -v --timeout 150 --timeout-method thread > $OUT/tests.log 2>&1; rc=$?; echo "tests rc=$rc"; grep -E "FAIL|Error |error:|^E |passed|failed" $OUT/tests.log | head -30
+exit 0

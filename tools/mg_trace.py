@@ -53,8 +53,36 @@ def analyse(path, which=-3):
         print(f'{nm[:40]:40s} {c:4d} {t:9.1f}')
 
 
+def setup(path):
+    """Kernels of the last solve's set-up: from the kernel after the previous solve's last CG step
+    (the last k_cg_beta before the final k_cg_alpha run) to the first k_cg_alpha of the last solve."""
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r['Start_Timestamp']))
+    al = [i for i, r in enumerate(rows) if 'k_cg_alpha' in r['Kernel_Name']]
+    # solves are separated by a gap in alpha indices larger than one iteration's kernels
+    gaps = [(al[k + 1] - al[k], k) for k in range(len(al) - 1)]
+    big = max(gaps)[1]
+    i1 = al[big + 1]
+    i0 = al[big] + 1
+    while i0 < i1 and 'k_cg_beta' not in rows[i0]['Kernel_Name']:
+        i0 += 1
+    i0 += 1
+    tot = {}
+    for r in rows[i0:i1]:
+        nm = short(r['Kernel_Name'])
+        t = tot.setdefault(nm, [0, 0.0])
+        t[0] += 1
+        t[1] += (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
+    span = (int(rows[i1]['Start_Timestamp']) - int(rows[i0]['Start_Timestamp'])) / 1e3
+    print(f'set-up span {span:.1f} us, kernels {i1 - i0}, busy {sum(v[1] for v in tot.values()):.1f} us')
+    for nm, (c, t) in sorted(tot.items(), key=lambda kv: -kv[1][1])[:30]:
+        print(f'{nm[:40]:40s} {c:4d} {t:9.1f}')
+
+
 if __name__ == '__main__':
-    if sys.argv[1] == 'analyse':
+    if sys.argv[1] == 'setup':
+        setup(sys.argv[2])
+    elif sys.argv[1] == 'analyse':
         analyse(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else -3)
     else:
         run(sys.argv[1])
