@@ -40,7 +40,7 @@ def golden_kwargs(g):
     return ast.literal_eval(str(g['kwargs']))
 
 
-SYSTEMS = ['sf3d', 'sf3d_edit', 'nb_xt', 'nb_err']
+SYSTEMS = ['sf3d', 'sf3d_edit', 'nb_xt', 'nb_err', 'sf3d_eq_edit']
 
 
 @pytest.fixture(scope='session')

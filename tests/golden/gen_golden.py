@@ -189,6 +189,20 @@ def gen_systems(LS, stubs):
                                           VERBOSE=False, dzdt_lags=[1]))
 
 
+def gen_eq_edit(LS, stubs):
+    """Equal z0 / dz spacing (the BASELINE configs' layout) with outliers and 3 outer iterations
+    of editing: the structure on which smooth_fit runs the multigrid solver at scale."""
+    rng = np.random.default_rng(20251123)
+    W = {'x': 1800., 'y': 1500., 't': 1.5}
+    ctr = {'x': 0., 'y': 0., 't': 0.}
+    x, y, t, z = synth_points(rng, W, ctr, 1200)
+    bad = rng.random(x.size) > 0.92
+    z[bad] += (rng.random(bad.sum()) - 0.5) * 40
+    run_sf(LS, stubs, 'sf3d_eq_edit', {'x': x, 'y': y, 'time': t, 'z': z, 'sigma': np.full(x.size, 0.1)},
+           dict(W=W, ctr=ctr, spacing={'z0': 100., 'dz': 100., 'dt': 0.25}, E_RMS=E_RMS_NB,
+                reference_epoch=3, max_iterations=3, VERBOSE=False, dzdt_lags=[1]))
+
+
 def gen_avg(LS, stubs):
     """Averaging products (grid_functions.py:177-324, lin_op.py:347-488,669-732):
     avg_scales (dz and dz/dt per lag), z0_average_scale and a named avg_masks region, with
@@ -446,7 +460,8 @@ def main():
     sys.modules['LSsurf.smooth_fit'].smooth_fit   # module (LSsurf/__init__.py:6 rebinds the name)
     gens = {'stencils': lambda: gen_stencils(LS), 'tri': lambda: gen_tri(LS), 'lin2d': lambda: gen_lin2d(LS),
             'systems': lambda: gen_systems(LS, _refstubs), 'avg': lambda: gen_avg(LS, _refstubs),
-            'kat': lambda: gen_kat(LS), 'aniso': lambda: gen_aniso(LS, _refstubs)}
+            'kat': lambda: gen_kat(LS), 'aniso': lambda: gen_aniso(LS, _refstubs),
+            'eq_edit': lambda: gen_eq_edit(LS, _refstubs)}
     for name in (sys.argv[1:] or list(gens)):   # e.g. `gen_golden.py aniso`: only those fixtures
         gens[name]()
 

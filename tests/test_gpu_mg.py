@@ -72,7 +72,7 @@ def test_mg_vcycle_is_spd(gpu_available):
     assert u @ Vu > 0 and v @ Vv > 0
 
 
-@pytest.mark.parametrize('name', ['sf3d', 'sf3d_edit', 'nb_xt', 'nb_err'])
+@pytest.mark.parametrize('name', ['sf3d', 'sf3d_eq_edit', 'sf3d_edit', 'nb_xt', 'nb_err'])
 def test_mg_pcg_matches_exact_solution(gpu_available, name):
     """sf3d: z0 and dz on one lattice; sf3d_edit / nb_xt / nb_err: z0 on a 2× refinement of the dz
     lattice (the notebooks' z0 50 m / dz 100 m) — the hierarchy starts with the z0-refined level."""

@@ -47,6 +47,26 @@ def test_outer_editing_loop(gpu_available):
     assert S['timing']['lsq_iters'] > 0
 
 
+@pytest.mark.parametrize('name,precond', [('sf3d_eq_edit', 'auto'), ('sf3d_eq_edit', 4), ('sf3d_edit', 4)])
+def test_editing_loop_solvers(gpu_available, name, precond):
+    """The outer editing loop (3 / 4 outer iterations, outliers) with the default solver and with
+    the multigrid-preconditioned CGNR forced (lsq_precond=4: equal spacing — the BASELINE configs'
+    layout — and z0 on a 2× refinement of dz) reproduces the reference's edits and outputs."""
+    g = golden(f'sys_{name}.npz')
+    kw = golden_kwargs(g)
+    S = LS.smooth_fit(data=golden_points(g), lsq_precond=precond, **kw)
+    tse = S['data'].three_sigma_edit
+    flips = np.sum(tse != g['data_three_sigma_edit'].astype(bool))
+    assert flips <= 2
+    if precond == 4:
+        assert S['timing']['lsq_last']['method'] == 1
+    if flips == 0:
+        assert _rel(S['m']['z0'].z0, g['z0']) < 1e-6
+        assert _rel(S['m']['dz'].dz, g['dz']) < 1e-6
+        assert _rel(S['data'].sigma_extra, g['data_sigma_extra']) < 1e-5
+        assert _rel(S['data'].z_est, g['data_z_est']) < 1e-6
+
+
 def test_notebook_amplitude_kat(gpu_available):
     k = golden('kat.npz')
     from lssurf_amd import containers as pc
