@@ -137,9 +137,10 @@ __global__ __launch_bounds__(BLOCK) void k_band_width(int64_t m, const int64_t* 
         if (rs[i] == 0.0) continue;
         int lo = INT_MAX, hi = -1;
         for (int64_t f = rp[i]; f < rp[i + 1]; ++f) {
-            const int t = pinv[ci[f]] >> 6;
-            lo = min(lo, t);
-            hi = max(hi, t);
+            const int k = pinv[ci[f]];
+            if (k < 0) continue;   // a column outside the window (lsq_cov_band_window)
+            lo = min(lo, k >> 6);
+            hi = max(hi, k >> 6);
         }
         if (hi >= 0) local = max(local, hi - lo);
     }
@@ -445,6 +446,9 @@ __global__ __launch_bounds__(BLOCK) void k_band_sweep(BandDev b, int64_t j0, con
             ss[((c & 31) >= 16) ? 1 : 0] += v * v;
         });
         __threadfence();
+        // the next step's first ring load (before its loop's barrier) may read this very slot
+        // (step K0 + 1 reads Y_K0): every thread's stores must have landed
+        __syncthreads();
     }
     // column sums: thread (wave wv, lane) holds columns c0 + 16t + (lane&15) over rows lk + 4g (+16s)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -756,23 +760,27 @@ void run_sweeps(hipStream_t st, const BandDev& b, int64_t nwg, int64_t cap, cons
 
 // AᵀA of the current weighted, masked system in the order h_perm (nullable: natural), equilibrated
 // and factored inside its band into F
-void band_factor(System& S, const int32_t* h_perm, BandFactor& F) {
+// nw ≥ 0: the first nw entries of h_perm are a WINDOW of the columns; the factor is that of the
+// principal submatrix (AᵀA)_WW = A_WᵀA_W (every other column held fixed)
+void band_factor(System& S, const int32_t* h_perm, BandFactor& F, int64_t nw) {
     hipStream_t st = S.stream;
-    const int64_t n = S.G.n;
+    const int64_t ncol = S.G.n;
+    const int64_t n = nw >= 0 ? nw : ncol;
     if (n <= 0) throw std::invalid_argument("band factor: empty system");
     if (n >= INT_MAX) throw std::invalid_argument("band factor: too many columns");
-    std::vector<int32_t> pinv(n, -1), perm(n);
+    if (nw >= 0 && (!h_perm || nw > ncol)) throw std::invalid_argument("band factor: bad window");
+    std::vector<int32_t> pinv(ncol, -1), perm(n);
     for (int64_t j = 0; j < n; ++j) {
         const int32_t o = h_perm ? h_perm[j] : (int32_t)j;
-        if (o < 0 || o >= n || pinv[o] >= 0) throw std::invalid_argument("band factor: the order is not a permutation of the columns");
+        if (o < 0 || o >= ncol || pinv[o] >= 0) throw std::invalid_argument("band factor: the order is not a permutation of the columns");
         pinv[o] = (int32_t)j;
         perm[j] = o;
     }
     const int64_t T = (n + TB - 1) / TB, npad = T * TB;
-    DBuf<int32_t> dpinv(n);
+    DBuf<int32_t> dpinv(ncol);
     F.perm.alloc(n);
     F.perm.upload(perm.data(), n, st);
-    dpinv.upload(pinv.data(), n, st);
+    dpinv.upload(pinv.data(), ncol, st);
     DBuf<int> wmax(1);
     wmax.zero(st);
     hipLaunchKernelGGL(k_band_width, dim3(grid_for(S.G.m)), dim3(BLOCK), 0, st, S.G.m, S.G.rp.p, S.G.ci.p, dpinv.p,
@@ -933,25 +941,28 @@ void band_factor_download(System& S, const int32_t* h_perm, int64_t* info, doubl
     HIP_CHECK(hipStreamSynchronize(S.stream));
 }
 
-void band_cov(System& S, const int32_t* h_perm, double* h_E, int64_t nops, const int64_t* h_rp, const int32_t* h_ci,
-              const double* h_v, double* h_oe, int64_t* info) {
+void band_cov(System& S, const int32_t* h_perm, int64_t nw, double* h_E, int64_t nops, const int64_t* h_rp,
+              const int32_t* h_ci, const double* h_v, double* h_oe, int64_t* info) {
     hipStream_t st = S.stream;
     refresh_scaling(S, S.cs_mode < 0 ? 0 : S.cs_mode);
-    const int64_t n = S.G.n;
+    const int64_t ncol = S.G.n;
     for (int64_t i = 0; i < nops; ++i)
         for (int64_t e = h_rp[i]; e < h_rp[i + 1]; ++e)
-            if (h_ci[e] < 0 || h_ci[e] >= n) throw std::invalid_argument("lsq_cov_band: op column out of range");
+            if (h_ci[e] < 0 || h_ci[e] >= ncol) throw std::invalid_argument("lsq_cov_band: op column out of range");
     BandFactor F;
-    band_factor(S, h_perm, F);
-    const int64_t T = F.T, npad = T * TB;
+    band_factor(S, h_perm, F, nw);
+    const int64_t n = F.n, T = F.T, npad = T * TB;
     const int w = F.w;
-    std::vector<int32_t> pinv(n);
+    std::vector<int32_t> pinv(ncol, -1);
     {
         std::vector<int32_t> perm(n);
         F.perm.download(perm.data(), n, st);
         HIP_CHECK(hipStreamSynchronize(st));
         for (int64_t j = 0; j < n; ++j) pinv[perm[j]] = (int32_t)j;
     }
+    for (int64_t i = 0; i < nops; ++i)
+        for (int64_t e = h_rp[i]; e < h_rp[i + 1]; ++e)
+            if (pinv[h_ci[e]] < 0) throw std::invalid_argument("lsq_cov_band_window: an op row reaches outside the window");
     BandDev b{T, w, F.R.p, F.D.p};
     const int64_t ring_wg = (int64_t)(w + 1) * TT * (int64_t)sizeof(double);
     const int64_t bytes = (T * (int64_t)(w + 1) + T) * TT * (int64_t)sizeof(double) + npad * 16;
@@ -966,11 +977,12 @@ void band_cov(System& S, const int32_t* h_perm, double* h_E, int64_t nops, const
     const int64_t cap = std::min<int64_t>({(int64_t)(0.5 * avail / ring_wg), std::max(T, nop_wg), 1 << 16});
     DBuf<double> ring(cap * (w + 1) * TT);
     // the diagonal: identity right-hand sides, tile J from row J on
-    DBuf<double> ssq(npad), dE(n);
+    DBuf<double> ssq(npad), dE(ncol);
+    if (n < ncol) dE.zero(st);   // a window: the other columns 0
     run_sweeps<true>(st, b, T, cap, nullptr, nullptr, nullptr, nullptr, nullptr, F.sc.p, ring.p, ssq.p);
     hipLaunchKernelGGL(k_band_diag_sweep, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, F.perm.p, ssq.p, F.sc.p, dE.p);
     KERNEL_CHECK();
-    dE.download(h_E, n, st);
+    dE.download(h_E, ncol, st);
     HIP_CHECK(hipStreamSynchronize(st));
     int64_t products = 0;
     for (int64_t J = 0; J < T; ++J) products += (T - J) * (int64_t)std::min<int64_t>(w + 1, T - J);

@@ -428,7 +428,7 @@ void build_dmf(System& S, int32_t n_grids, const lsq_grid_desc* grids, int32_t n
 void ensure_sell(System& S);                    // assembled A / AT (lazy when S.mf)
 void refresh_scaling(System& S, int precond);
 // band.hip: sqrt(diag((AᵀA)⁻¹)) and op-row variances from a banded Cholesky + Takahashi inverse
-void band_factor(System& S, const int32_t* perm, BandFactor& F);
+void band_factor(System& S, const int32_t* perm, BandFactor& F, int64_t nw = -1);   // nw ≥ 0: a column window
 void graph_cache_drop(const System* S);   // lsqr.hip: captured iteration batches of S
 void band_solve_scratch(System& S);
 void band_precond(System& S);   // S.band from S.band_order (precond 5)
@@ -438,7 +438,7 @@ void band_launch_warm(System& S, const double* x0, double* y0);
 void band_check(System& S);   // throws when a precond-5 solve's grid barrier timed out
 void band_factor_download(System& S, const int32_t* perm, int64_t* info, double* R_out, double* sc_out,
                           int32_t* perm_out);   // sparseqr.rz drop-in (lsq_band_factor)
-void band_cov(System& S, const int32_t* perm, double* E, int64_t nops, const int64_t* rp, const int32_t* ci,
+void band_cov(System& S, const int32_t* perm, int64_t nw, double* E, int64_t nops, const int64_t* rp, const int32_t* ci,
               const double* v, double* op_err, int64_t* info);   // rs/cs -> SELL values (single GPU)
 void scaling_rows_colnorm(System& S, int precond, bool raw);
 void mf_column_scale(System& S, bool raw);       // lsqr.hip: column norms from the stencil structure

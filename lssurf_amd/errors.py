@@ -14,6 +14,17 @@ Default (`method='band'`): no dense factor — the columns are ordered by node p
 sweeps without being stored (liblsqsurf `lsq_cov_band`, csrc/band.hip); the averaging operators'
 errors sqrt(diag(op (AᵀA)⁻¹ opᵀ)) come from sweeps with the op rows as right-hand sides.
 `method='dense'` keeps the n × n factor and R⁻¹ (n ≲ 3·10⁴).
+
+At scale (`method='window'`, and `'auto'` above WINDOW_MIN_COLS columns): the band of AᵀA grows
+with the lattice width (O(n·w²) work, O(n·w) memory: infeasible past ~2·10⁵ columns).  (AᵀA)⁻¹'s
+correlations decay with node distance (measured: |corr| 0.30 / 0.11 / 0.03 / 0.018 at 2 / 4 / 6 /
+8 nodes, t64-type systems), so diag((AᵀA)⁻¹) of the nodes of a tile is that of the principal
+submatrix over the tile plus a margin of nodes — the variance conditional on the columns outside
+held fixed differs from the marginal one by the correlations across the margin.  Tiles of
+`tile` × `tile` nodes of the (coarser) dz lattice, windows of ± `margin` nodes, each factored in
+its band on the device (lsq_cov_band_window); the averaging operators' rows go with the tile of
+their support's centre (their support must lie inside the window).  Accuracy against the full
+band factor: DESIGN.md §Error propagation (tests/test_gpu_errors_window.py).
 """
 from time import time
 
@@ -42,6 +53,86 @@ def band_order(grids, keep_cols):
     return np.lexsort((k[3], k[2], k[1], k[0])).astype(np.int32)
 
 
+WINDOW_MIN_COLS = 250_000      # 'auto': the full band below, tiled windows above
+WINDOW_TILE, WINDOW_MARGIN = 64, 24   # σ within ~3e-6 of the full band at 128²×12 (tests)
+
+
+def _node_index(grids, keep_cols):
+    """(iy, ix, dy, dx) per compact column: node indices on the coarsest (y, x) lattice of the grids
+    (a finer z0 node maps to the coarse cell it lies in) and that lattice's spacing."""
+    gl = [g for g in grids.values() if getattr(g, 'N_dims', 0) >= 2]
+    n_full = max(int(g.col_N) for g in gl)
+    dy = max(float(g.delta[0]) for g in gl)
+    dx = max(float(g.delta[1]) for g in gl)
+    y0 = min(float(g.ctrs[0][0]) for g in gl)
+    x0 = min(float(g.ctrs[1][0]) for g in gl)
+    iy = np.zeros(n_full, np.int64)
+    ix = np.zeros(n_full, np.int64)
+    for g in gl:
+        sub = np.unravel_index(np.arange(int(g.N_nodes)), tuple(g.shape))
+        idx = np.arange(g.col_0, g.col_0 + int(g.N_nodes))
+        iy[idx] = np.floor((g.ctrs[0][sub[0]] - y0) / dy + 1e-9).astype(np.int64)
+        ix[idx] = np.floor((g.ctrs[1][sub[1]] - x0) / dx + 1e-9).astype(np.int64)
+    return iy[keep_cols], ix[keep_cols]
+
+
+def window_cov(solver, grids, keep_cols, op=None, tile=WINDOW_TILE, margin=WINDOW_MARGIN, timing=None):
+    """(E, op_err) of the current weighted, masked system by tiled windows (module docstring):
+    E[c] ≈ sqrt(((AᵀA)⁻¹)_cc) per compact column, op_err[i] ≈ sqrt(op_i (AᵀA)⁻¹ op_iᵀ)."""
+    iy, ix = _node_index(grids, keep_cols)
+    order = band_order(grids, keep_cols)
+    n = iy.size
+    E = np.zeros(n)
+    op_err = None
+    ny, nx = int(iy.max()) + 1, int(ix.max()) + 1
+    iy_o, ix_o = iy[order], ix[order]
+    if op is not None:   # every op row with its support's node box; rows go with the tile of its centre
+        op = sp.csr_matrix(op)
+        op_err = np.zeros(op.shape[0])
+        nr = op.shape[0]
+        rows_of = np.repeat(np.arange(nr), np.diff(op.indptr))
+        big = np.iinfo(np.int64).max
+        y_lo = np.full(nr, big); y_hi = np.full(nr, -1); x_lo = np.full(nr, big); x_hi = np.full(nr, -1)
+        np.minimum.at(y_lo, rows_of, iy[op.indices]); np.maximum.at(y_hi, rows_of, iy[op.indices])
+        np.minimum.at(x_lo, rows_of, ix[op.indices]); np.maximum.at(x_hi, rows_of, ix[op.indices])
+        empty = y_hi < 0
+        y_lo[empty] = y_hi[empty] = x_lo[empty] = x_hi[empty] = 0
+        oty, otx = (y_lo + y_hi) // 2 // tile, (x_lo + x_hi) // 2 // tile
+        # rows whose support leaves their tile's window get windows of their own (support ± margin)
+        own = (y_lo < oty * tile - margin) | (y_hi >= oty * tile + tile + margin) | \
+              (x_lo < otx * tile - margin) | (x_hi >= otx * tile + tile + margin)
+
+    def run(win, inner, rows):
+        sub = op[rows] if rows is not None and rows.size else None
+        Et, oe, info = solver.cov_band_window(order[win], sub)
+        if inner is not None:
+            E[inner] = Et[inner]
+        if sub is not None:
+            op_err[rows] = oe
+        return int(info[0])
+
+    ntiles = nown = 0
+    wmax = 0
+    for ty in range(0, ny, tile):
+        for tx in range(0, nx, tile):
+            win = (iy_o >= ty - margin) & (iy_o < ty + tile + margin) & (ix_o >= tx - margin) & (ix_o < tx + tile + margin)
+            inner = (iy >= ty) & (iy < ty + tile) & (ix >= tx) & (ix < tx + tile)
+            rows = None if op is None else np.flatnonzero((oty == ty // tile) & (otx == tx // tile) & ~own)
+            wmax = max(wmax, run(win, inner, rows))
+            ntiles += 1
+    if op is not None and own.any():   # one window per distinct support box
+        boxes = np.stack([y_lo, y_hi, x_lo, x_hi], axis=1)
+        for b in np.unique(boxes[own], axis=0):
+            rows = np.flatnonzero(own & np.all(boxes == b, axis=1))
+            win = (iy_o >= b[0] - margin) & (iy_o <= b[1] + margin) & (ix_o >= b[2] - margin) & (ix_o <= b[3] + margin)
+            wmax = max(wmax, run(win, None, rows))
+            nown += 1
+    if timing is not None:
+        timing['E_window'] = {'tiles': ntiles, 'op_windows': nown, 'tile': tile, 'margin': margin,
+                              'max_band_tiles': wmax}
+    return E, op_err
+
+
 def _compact_rows(op, keep_cols, n_full):
     """The op's CSR (rows = its output equations) over the compact columns: entries in removed
     columns dropped (Ip_c·Rinv has zero rows there, smooth_fit.py:266)."""
@@ -59,7 +150,7 @@ def _grid_values(op, vals):
 
 
 def calc_and_parse_errors(E, G_data, Gc, Ed, Ec, data, in_TSE, keep_cols, grids, avg_ops, device=0, timing=None,
-                          method='band'):
+                          method='auto'):
     timing = {} if timing is None else timing
     tic = time()
     sigma_data = np.sqrt(Ed ** 2 + data.sigma_extra ** 2)
@@ -70,7 +161,21 @@ def calc_and_parse_errors(E, G_data, Gc, Ed, Ec, data, in_TSE, keep_cols, grids,
     try:
         fs.solver.set_row_weight(w)
         fs.solver.set_row_mask(np.concatenate([np.asarray(in_TSE, bool), np.ones(Gc.N_eq, bool)]))
-        if method == 'band':
+        if method == 'auto':
+            method = 'band' if keep_cols.size <= WINDOW_MIN_COLS else 'window'
+        if method == 'window':
+            keys = list(avg_ops)
+            mats = [_compact_rows(avg_ops[k], keep_cols, Gc.col_N) for k in keys]
+            op = sp.vstack(mats).tocsr() if mats else None
+            E0c, errs = window_cov(fs.solver, grids, keep_cols, op, tile=WINDOW_TILE, margin=WINDOW_MARGIN,
+                                   timing=timing)
+            timing['decompose_qz'] = time() - tic
+            off = 0
+            for k, m in zip(keys, mats):
+                op_err[k] = errs[off:off + m.shape[0]]
+                off += m.shape[0]
+            Rinv = None
+        elif method == 'band':
             keys = list(avg_ops)
             mats = [_compact_rows(avg_ops[k], keep_cols, Gc.col_N) for k in keys]
             op = sp.vstack(mats).tocsr() if mats else None

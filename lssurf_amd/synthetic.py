@@ -21,6 +21,7 @@ CONFIGS = {
     # small ones for tests / smoke
     't64': (64, 12, 8_192),
     't256': (256, 12, 131_072),
+    't128': (128, 12, 32_768),
     'tdense': (64, 12, 40_000),   # ~10 points per cell: strips whose point runs overflow LDS staging
     't15': (80, 15, 12_000),        # 15 epochs: the 16-long register columns; 80 nodes: two strips per row
     # one rank's window of C4 over 4 / 8 GPUs (owned node rows + 2 halo rows, 1/N of the points):

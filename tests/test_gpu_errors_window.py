@@ -1,0 +1,83 @@
+"""compute_E at scale: diag((AᵀA)⁻¹) by tiled windows (errors.window_cov,
+lsq_cov_band_window) against the full band factor (lsq_cov_band) and the dense path.
+
+* the full band factor is deterministic and equals the dense inverse at 64²×12 (≤ 1e-11) — a
+  round-2 race in its sweeps (a workgroup's second step read the ring tile its first step had just
+  written, without a barrier) made it differ by up to 100 % between calls at this size;
+* tiles of 16 / 32 nodes with a 16 / 24-node margin: σ within 5e-4 / 1e-5 (max) of the full band
+  at 64² / 128²×12 — the conditional variance given the columns outside the window, whose
+  correlations with the tile decay with distance (DESIGN.md §Error propagation);
+* averaging operators' errors through the windows (sys_avg golden system, tiles smaller than its
+  grid, operators wider than a tile in windows of their own) within 1e-5 of the exact ones."""
+import numpy as np
+import pytest
+
+import lssurf_amd as LS
+from conftest import golden, golden_avg_masks, golden_kwargs, golden_points
+
+pytestmark = pytest.mark.gpu
+
+
+def _system(name):
+    from lssurf_amd import synthetic
+    from lssurf_amd.constraint_functions import reference_epoch_keep_cols
+    from lssurf_amd.smooth_fit import FitSystem
+    D, kw = synthetic.points(name)
+    S = LS.smooth_fit(data=D, return_fit_objects=True, VERBOSE=False, **kw)
+    keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch'])
+    fs = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, grids=S['grids'])
+    w = 1. / np.concatenate((S['Ed'], S['Ec']))
+    fs.solver.set_row_weight(w)
+    fs.solver.set_row_mask(np.ones(w.size, bool))
+    return S, fs, keep
+
+
+def test_band_covariance_deterministic_and_exact(gpu_available):
+    from lssurf_amd.errors import band_order
+    S, fs, keep = _system('t64')
+    try:
+        o = band_order(S['grids'], keep)
+        E1, _, _ = fs.solver.cov_band(o)
+        E2, _, _ = fs.solver.cov_band(o)
+        Ed = fs.solver.sigma_x()
+    finally:
+        fs.close()
+    np.testing.assert_array_equal(E1, E2)
+    assert np.max(np.abs(E1 - Ed) / Ed) <= 1e-11
+
+
+@pytest.mark.parametrize('name,tile,margin,tol_max,tol_p99', [('t64', 16, 16, 5e-4, 3e-5),
+                                                               ('t128', 32, 24, 1e-5, 1e-7)])
+def test_window_covariance_matches_full_band(gpu_available, name, tile, margin, tol_max, tol_p99):
+    """Measured (one box): margin 16 — max 7.6e-5 (64²) / 3.5e-4 (128²), 99th percentile 1.1e-5 /
+    1.3e-5; margin 24 (the default) — max 3.1e-6, 99th percentile 7.8e-8 at 128²×12."""
+    from lssurf_amd.errors import band_order, window_cov
+    S, fs, keep = _system(name)
+    try:
+        Ef, _, _ = fs.solver.cov_band(band_order(S['grids'], keep))
+        Ew, _ = window_cov(fs.solver, S['grids'], keep, tile=tile, margin=margin)
+    finally:
+        fs.close()
+    rel = np.abs(Ew - Ef) / Ef
+    assert rel.max() <= tol_max, rel.max()
+    assert np.quantile(rel, 0.99) <= tol_p99, np.quantile(rel, 0.99)
+
+
+def test_window_averaging_errors(gpu_available):
+    """smooth_fit(compute_E=True, lsq_E_method='window') with tiles smaller than the grid: the
+    z0 / dz σ grids and the averaging products' errors against the reference's exact ones."""
+    from lssurf_amd import errors
+    g = golden('sys_avg.npz')
+    saved = errors.WINDOW_TILE, errors.WINDOW_MARGIN
+    errors.WINDOW_TILE, errors.WINDOW_MARGIN = 8, 16
+    try:
+        S = LS.smooth_fit(data=golden_points(g), avg_masks=golden_avg_masks(g), lsq_E_method='window',
+                          **golden_kwargs(g))
+    finally:
+        errors.WINDOW_TILE, errors.WINDOW_MARGIN = saved
+    assert S['timing']['E_window']['tiles'] > 1
+    rel = lambda a, b: np.nanmax(np.abs(np.asarray(a) - b) / np.abs(b))
+    keys = [k[4:] for k in g.files if k.startswith('avg_')]
+    for k in keys:
+        E = getattr(S['E']['sigma_' + k], 'sigma_' + k)
+        assert rel(E, g['Eexact_sigma_' + k]) < 1e-5, k
