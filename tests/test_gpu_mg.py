@@ -212,3 +212,39 @@ def test_mg_z0_refined_iterations(gpu_available):
     assert st['method'] == 1 and st['istop'] in (1, 2), st
     assert np.linalg.norm(xm - xb) / np.linalg.norm(xb) <= 1e-8
     assert st['iters'] * 4 <= it_bj, (st['iters'], it_bj)
+
+
+_PERSIST_CHILD = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from test_gpu_cgnr import _synthetic_system, TOL
+S, fs, w, rhs = _synthetic_system('t64')
+try:
+    x = fs.solve(w, np.ones(fs.n_data, bool), rhs, precond=4, method=1, **TOL)
+    np.save(sys.argv[2], np.concatenate([[fs.stats['iters']], x]))
+finally:
+    fs.close()
+'''
+
+
+def test_mg_persistent_coarse_levels(gpu_available, tmp_path):
+    """k_mg_coarse (the small coarse levels in one persistent launch with grid barriers; off by
+    default, LSQ_MG_PERSIST) gives the launch-per-kernel V-cycle's solve: run in a child process
+    with it on (t64: levels 33², 17², 9²), compared with this process's default."""
+    import os
+    import subprocess
+    import sys
+    out = tmp_path / 'x.npy'
+    env = dict(os.environ, LSQ_MG_PERSIST='16384', LSQ_MG_PWG='32')
+    r = subprocess.run([sys.executable, '-c', _PERSIST_CHILD, os.path.dirname(__file__), str(out)], env=env,
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = np.load(out)
+    S, fs, w, rhs = _synthetic_system('t64')
+    try:
+        x = fs.solve(w, np.ones(fs.n_data, bool), rhs, precond=4, method=1, **TOL)
+        it = fs.stats['iters']
+    finally:
+        fs.close()
+    assert abs(int(got[0]) - it) <= 1, (got[0], it)
+    assert np.linalg.norm(got[1:] - x) <= 1e-8 * np.linalg.norm(x)
