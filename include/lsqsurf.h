@@ -65,6 +65,9 @@ typedef struct lsq_opts {
     int32_t op;            /* operator the iteration streams: 0 = auto (the structured stencil  */
                            /*     operator when the matrix came from lsq_set_matrix_stencil and */
                            /*     precond < 2; else assembled SELL), 1 = assembled SELL always  */
+    int64_t b_rows;        /* rows of b that may be non-zero: b[0, b_rows) is uploaded, the     */
+                           /*     rest taken as zero (smooth_fit: the data rows, when no prior  */
+                           /*     is non-zero); 0 = all m rows                                 */
 } lsq_opts;
 
 /* Statistics (mirrors scipy's lsqr return tuple, plus timing and the byte model). */

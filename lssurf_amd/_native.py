@@ -22,7 +22,7 @@ class LsqOpts(ctypes.Structure):
     _fields_ = [('method', ctypes.c_int32), ('precond', ctypes.c_int32), ('atol', ctypes.c_double),
                 ('btol', ctypes.c_double), ('conlim', ctypes.c_double), ('maxit', ctypes.c_int64),
                 ('use_x0', ctypes.c_int32), ('batch', ctypes.c_int32), ('use_graph', ctypes.c_int32),
-                ('op', ctypes.c_int32)]
+                ('op', ctypes.c_int32), ('b_rows', ctypes.c_int64)]
 
 
 class GridDesc(ctypes.Structure):

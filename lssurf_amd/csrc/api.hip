@@ -304,6 +304,7 @@ int lsq_solve(lsq_handle* h, const double* b, double* x_inout, const lsq_opts* o
         if (o->method == 1 && lsq::cg_available(S, o->precond)) {   // builds block factors / levels when stale
             HIP_CHECK(hipStreamSynchronize(S.stream));
             const double prep_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_prep).count();
+            if (getenv("LSQ_SETUP_TRACE")) fprintf(stderr, "setup %-16s %8.3f ms\n", "prepare", prep_s * 1e3);
             const int rc = lsq::cg_solve(S, b, x_inout, *o, s);
             if (s) s->setup_s += prep_s;
             return rc;

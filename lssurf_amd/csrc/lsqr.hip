@@ -524,6 +524,17 @@ void launch_flush(System& S, const Grids& g, bool mf) {
 
 }  // namespace
 
+// b on the device for a solve: rows [0, b_rows) from the host, the rest zero (lsq_opts.b_rows;
+// C4's b is 75 M rows of which the 2 M data rows are non-zero: uploading it whole from pageable
+// memory was most of the per-solve set-up), into the persistent S.rhs
+const double* upload_rhs(System& S, const double* h_b, const lsq_opts& o, hipStream_t st) {
+    const int64_t m = S.G.m, nb = o.b_rows > 0 && o.b_rows < m ? o.b_rows : m;
+    if (S.rhs.n < std::max<int64_t>(m, 1)) S.rhs.alloc(std::max<int64_t>(m, 1));
+    S.rhs.upload(h_b, nb, st);
+    if (nb < m) HIP_CHECK(hipMemsetAsync(S.rhs.p + nb, 0, (size_t)(m - nb) * sizeof(double), st));
+    return S.rhs.p;
+}
+
 // Initialise the LSQR state from rhs b (host, length m, unweighted) and optional warm start
 // x0 (host, length n, or nullptr).  Mirrors scipy lsqr's set-up block for the operator A·M
 // (M = diag(cs) for precond 0/1, M = R⁻¹ for precond 2).
@@ -534,9 +545,8 @@ void lsqr_init_mf(System& S, const double* h_b, const double* h_x0, const lsq_op
     hipStream_t st = S.stream;
     ensure_workspace(S);
     const Grids g = grids_for(S);
-    const int64_t m = S.G.m, n = S.G.n, nf = S.n_full;
-    DBuf<double> db(std::max<int64_t>(m, 1));
-    db.upload(h_b, m, st);
+    const int64_t n = S.G.n, nf = S.n_full;
+    const double* dbp = upload_rhs(S, h_b, o, st);
     DBuf<double> dx0, dy0, dz0;
     if (h_x0) {
         dx0.alloc(std::max<int64_t>(n, 1));
@@ -562,7 +572,7 @@ void lsqr_init_mf(System& S, const double* h_b, const double* h_x0, const lsq_op
     h.cs2 = -1.0;
     HIP_CHECK(hipMemcpyAsync(S.st.p, &h, sizeof(h), hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_mf_init_u_for(S), dim3(g.gD + g.gS), dim3(BLOCK), 0, st, g.gD, S.mfh.npts, S.Ad.nslices, S.Ad.sp.p,
-                       S.Ad.ci.p, S.Ad.val.p, S.Ad.perm.p, S.mfd.p, h_x0 ? dz0.p : nullptr, S.rs.p, db.p, S.u.p, S.bw.p,
+                       S.Ad.ci.p, S.Ad.val.p, S.Ad.perm.p, S.mfd.p, h_x0 ? dz0.p : nullptr, S.rs.p, dbp, S.u.p, S.bw.p,
                        S.part_u.p, S.part_b.p);
     KERNEL_CHECK();
     hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gD + g.gS, S.part_b.p,
@@ -598,8 +608,7 @@ void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts&
     const Grids g = grids_for(S);
     const int64_t m = S.G.m, n = S.G.n;
     const bool dense = o.precond == 2, block = o.precond == 3, band = o.precond == 5;
-    DBuf<double> db(std::max<int64_t>(m, 1));
-    db.upload(h_b, m, st);
+    const double* dbp = upload_rhs(S, h_b, o, st);
     DBuf<double> dx0, dy0;
     if (h_x0) {
         dx0.alloc(std::max<int64_t>(n, 1));
@@ -629,7 +638,7 @@ void lsqr_init(System& S, const double* h_b, const double* h_x0, const lsq_opts&
     // the SpMV of the warm start gathers in A·M coordinates: y0 for precond 0/1, x0 for 2 and 3
     const double* gather0 = h_x0 ? ((dense || block || band) ? dx0.p : dy0.p) : nullptr;
     hipLaunchKernelGGL(k_init_u, dim3(g.gA), dim3(BLOCK), 0, st, m, S.A.nslices, S.A.sp.p, S.A.ci.p, S.A.val.p,
-                       S.rs.p, db.p, gather0, S.A.perm.p, S.u.p, S.bw.p, S.part_u.p, S.part_b.p);
+                       S.rs.p, dbp, gather0, S.A.perm.p, S.u.p, S.bw.p, S.part_u.p, S.part_b.p);
     KERNEL_CHECK();
     hipLaunchKernelGGL(k_beta, dim3(1), dim3(BLOCK), 0, st, S.st.p, S.part_u.p, g.gA, S.part_b.p, g.gA, 1, nullptr);
     KERNEL_CHECK();

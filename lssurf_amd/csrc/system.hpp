@@ -181,6 +181,9 @@ struct CgGrid {
     int32_t gl[CG_MAX_GRP];                  // in-row LDS offset dx·tpad of group g
     int32_t gdx[CG_MAX_GRP];                 // dim-1 offset dx of group g (multigrid tile kernel)
     int32_t gc[CG_MAX_GRP];                  // offset of group g's MAXT × (2·DT_g + 1) coefficients in a row
+    // wave-strip operator (lsqr_cg_rw.inc): strips of rw_sx dim-1 positions × rw_ry rows, rw_nsx ×
+    // rw_nry of them, rw_chunk per XCD; its class table (per dim-0 class) from coefc[rwc0]
+    int32_t rw_sx, rw_nsx, rw_ry, rw_nry, rw_chunk, rwc0;
 };
 struct BlkAffine {
     int64_t base[16], stride[16];
@@ -223,6 +226,7 @@ struct CgDesc {
     int32_t nedge, maxt3, pad[2];            // column mode: workgroups of the CG iteration's k_cg_xedge (pad[0]: <8>;
                                              // pad[1]: lanes per item of the CG iteration's pass, 1 or 8); 3-D column length
     int32_t w8, pad2;                        // column mode: the CG iteration runs k_cg_normal_col8 (8-wave workgroups)
+    int32_t rw, rw_nwg;                      // the wave-strip operator k_cg_normal_rw applies; its workgroups
     CgGrid g[MF_MAX_GRIDS];
 };
 // CGNR data rows without a stored matrix (lsqr_cg.inc, k_cg_dmf_*): when every interpolation
@@ -387,6 +391,7 @@ struct System {
 
     // LSQR workspace
     DBuf<double> u, vb0, vb1, w, y, bw, zt, tt;
+    DBuf<double> rhs;          // b of the current solve (persistent: no per-solve allocation)
     DBuf<double> part_u, part_v, part_w, part_b;
     DBuf<LsqState> st;
     bool iter_ready = false;   // lsq_iterate state initialised

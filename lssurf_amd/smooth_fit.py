@@ -110,7 +110,7 @@ class FitSystem:
         if getattr(self, '_keep_last', None) is None or not np.array_equal(dk, self._keep_last):
             self.solver.set_row_mask(np.concatenate([dk, np.ones(self.n_con, dtype=bool)]))
             self._keep_last = dk.copy()
-        x, self.stats = self.solver.solve(rhs, x0=x0, **opts)
+        x, self.stats = self.solver.solve(rhs, x0=x0, b_rows=getattr(self, 'b_rows', 0), **opts)
         return x
 
     def expand(self, x):
@@ -431,13 +431,19 @@ def smooth_fit(**kwargs):
     np.divide(1., TCinv_diag, out=TCinv_diag)
     rhs = np.zeros([N_eq])
     rhs[0:data.size] = data.z.ravel()
+    b_rows = data.size   # rhs[b_rows:] == 0: only the data rows (and non-zero priors) cross PCIe
     for op in constraint_op_list:   # rhs[data.size:] = the concatenated priors
         if op.name not in zero_prior:
             rows = _as_slice(Gc.TOC['rows'][op.name])
+            prior = np.ravel(op.prior)
             if isinstance(rows, slice):
-                rhs[data.size + rows.start:data.size + rows.stop] = np.ravel(op.prior)
+                rhs[data.size + rows.start:data.size + rows.stop] = prior
+                end = rows.stop
             else:
-                rhs[data.size + rows] = np.ravel(op.prior)
+                rhs[data.size + rows] = prior
+                end = int(np.max(rows)) + 1 if np.size(rows) else 0
+            if np.any(prior != 0):
+                b_rows = max(b_rows, data.size + end)
     keep_cols = reference_epoch_keep_cols(G_data.col_N, grids['dz'], args['reference_epoch'])
     timing['setup'] = time() - tic
     in_TSE = data.three_sigma_edit > 0.01 if 'three_sigma_edit' in data.fields else np.ones(G_data.N_eq, dtype=bool)
@@ -457,6 +463,7 @@ def smooth_fit(**kwargs):
                 system = MultiDeviceFitSystem(G_data, Gc, keep_cols, Gc.col_N, devices)
             else:
                 system = FitSystem(G_data, Gc, keep_cols, Gc.col_N, device=devices[0], grids=grids)
+            system.b_rows = b_rows
             timing['device_setup'] = time() - tic
             tic_iteration = time()
             m0, sigma_extra, in_TSE, rs_data = iterate_fit(data, system, rhs, 1. / TCinv_diag, G_data, Gc, in_TSE,

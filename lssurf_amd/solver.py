@@ -133,27 +133,29 @@ class LSQSolver:
 
     # ---- solve -------------------------------------------------------------------------------
     def solve(self, b, x0=None, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, batch=0,
-              use_graph=True, op=0, method=0):
+              use_graph=True, op=0, method=0, b_rows=0):
         """LSQR (method 0) or CGNR (method 1: PCG on the normal equations with the fused
         normal-stencil operator; LSQR where that operator does not exist — stats['method'] says
         which ran); returns (x, stats) with scipy-lsqr-style stats (iters, istop, r1norm, ...).
         precond: 1 Jacobi, 2 dense Cholesky, 3 block-Jacobi per node, 4 multigrid V-cycle (CGNR
-        only).  batch 0: the library's default iterations per host convergence check."""
+        only).  batch 0: the library's default iterations per host convergence check.  b_rows > 0:
+        the caller guarantees b[b_rows:] == 0, so only b[:b_rows] crosses PCIe (smooth_fit: the
+        data rows; the 73 M constraint rows of C4 are zero)."""
         b = as_c(b, np.float64)
         if b.size != self.m:
             raise ValueError(f'b has {b.size} rows, system has {self.m}')
         x = np.zeros(self.n) if x0 is None else as_c(x0, np.float64).copy()
         o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond),
                          use_x0=int(x0 is not None), batch=int(batch), use_graph=int(bool(use_graph)), op=int(op),
-                         method=int(method))
+                         method=int(method), b_rows=int(b_rows))
         st = LsqStats()
         self._check(self._L.lsq_solve(self._h, ptr(b), ptr(x), ctypes.byref(o), ctypes.byref(st)), 'lsq_solve')
         return x, st.as_dict()
 
-    def iterate(self, b, iters, precond=1, batch=0, use_graph=True, op=0, method=0):
+    def iterate(self, b, iters, precond=1, batch=0, use_graph=True, op=0, method=0, b_rows=0):
         b = as_c(b, np.float64)
         o = default_opts(precond=int(precond), batch=int(batch), use_graph=int(bool(use_graph)), op=int(op),
-                         method=int(method))
+                         method=int(method), b_rows=int(b_rows))
         st = LsqStats()
         self._check(self._L.lsq_iterate(self._h, ptr(b), int(iters), ctypes.byref(o), ctypes.byref(st)),
                     'lsq_iterate')
@@ -180,7 +182,8 @@ class LSQSolver:
         self._check(self._L.lsq_profile_cg(self._h, int(reps), int(precond), ptr(o)), 'lsq_profile_cg')
         d = dict(zip(['cg_data', 'cg_normal', 'cg_update', 'cg_scalars'], o[:4].tolist()))
         d['bytes'] = {'cg_data': float(o[4]), 'cg_normal': float(o[5]), 'cg_update': float(o[6])}
-        d['data_rows'] = 'matrix-free' if o[7] else 'stored'
+        d['data_rows'] = 'matrix-free' if int(o[7]) & 1 else 'stored'
+        d['normal_kernel'] = 'wave-strip' if int(o[7]) & 2 else 'ring'
         return d
 
     def mg_info(self):
