@@ -100,7 +100,7 @@ class _Dist:
     def iterate(self, rhs, iters, op=0, precond=1, method=0):
         return self.ds.iterate(None, None, iters, precond=precond, method=method)
 
-    def solve(self, rhs, op=0, precond=1, method=0, b_rows=0):
+    def solve(self, rhs, op=0, precond=1, method=0):
         x = self.ds.solve(None, None, precond=precond, method=method)   # the single-GPU solve's tolerances
         return x, self.ds.stats
 
@@ -112,8 +112,7 @@ class _Dist:
             raise RuntimeError('lsq_profile_cg: ' + self.ds.L.lsq_last_error(self.ds.h).decode())
         d = dict(zip(['cg_data', 'cg_normal', 'cg_update', 'cg_scalars'], o[:4].tolist()))
         d['bytes'] = {'cg_data': float(o[4]), 'cg_normal': float(o[5]), 'cg_update': float(o[6])}
-        d['data_rows'] = 'matrix-free' if int(o[7]) & 1 else 'stored'
-        d['normal_kernel'] = 'wave-strip' if int(o[7]) & 2 else 'ring'
+        d['data_rows'] = 'matrix-free' if o[7] else 'stored'
         return d
 
     def profile_kernels(self, reps=10, op=0):
@@ -139,9 +138,8 @@ def cpu_baseline(fs, b_weighted, sample_iters, threads):
 # kernel symbols per role: LSQR (assembled-SELL operator / structured stencil operator), CGNR
 # (a role's launches per iteration: its PMC bytes are the sum over the symbols found)
 KERNEL_SYMBOL = {0: {'xw_spmv': ('k_xw_spmv(', 'k_mf_fwd('), 'spmtv': ('k_spmtv(', 'k_mf_spmtv(')},
-                 1: {'cg_data': ('k_cg_data(', 'k_cg_atdq(', 'k_cg_dmf_ad(', 'k_cg_ad_xedge<', 'k_cg_dmf_atq<'),
-                     'cg_normal': ('k_cg_normal(', 'k_cg_normal_col<', 'k_cg_normal_col8(', 'k_cg_normal_rw<',
-                                   'k_cg_xedge<'),
+                 1: {'cg_data': ('k_cg_data(', 'k_cg_atdq(', 'k_cg_dmf_ad(', 'k_cg_dmf_atq<'),
+                     'cg_normal': ('k_cg_normal(', 'k_cg_normal_col<', 'k_cg_xedge<'),
                      'cg_update': ('k_cg_block<', 'k_cg_jacobi(')}}
 
 
@@ -318,7 +316,6 @@ def main():
     # algorithmic bytes per launch (DESIGN.md §Byte model)
     kb = prof.pop('bytes')   # algorithmic bytes per launch, from the library's byte model
     data_rows = prof.pop('data_rows', None)   # CGNR: 'matrix-free' (points sorted by cell) or 'stored'
-    normal_kernel = prof.pop('normal_kernel', None)   # CGNR: 'wave-strip' (k_cg_normal_rw) or 'ring'
     dom = max(roles, key=lambda k: prof[k])
     achieved = kb[dom] / (prof[dom] * 1e-3) / 1e9
 
@@ -330,8 +327,6 @@ def main():
         # and (one GPU) LSQR + block-Jacobi for comparison
         names = {1: 'column scaling', 3: 'block-Jacobi per (y,x) node', 4: 'multigrid V-cycle (block-Jacobi smoothing)'}
         sp = args.precond
-        nzr = np.flatnonzero(rhs)   # b[b_rows:] == 0 (the constraint rows): only b[:b_rows] is uploaded
-        b_rows = int(nzr[-1]) + 1 if nzr.size else 0
         mg_ok = (getattr(fs, 'has_global', False) and fs.has_blocks) if isinstance(solver, _Dist) \
             else solver.cg_available(4)[0]
         if (args.solve_precond == 'auto' and meth == 1 and args.precond == 3 and mg_ok) or args.solve_precond == '4':
@@ -349,19 +344,15 @@ def main():
                                        if st['time_s'] > 0 else None,
                                        'frac': st['bytes_per_iter'] * st['iters'] / st['time_s'] / 1e9 / HBM_PEAK_GBS
                                        if st['time_s'] > 0 else None}}
-        # an untimed first solve: its set-up also captures and instantiates the iteration's hipGraph
-        # (host work once per system and preconditioner — smooth_fit's later outer iterations
-        # replay it); the timed solve's set-up is what every solve pays (factors, λ, first V-cycle)
-        _, sfirst = solver.solve(rhs, op=args.op, precond=sp, method=meth, b_rows=b_rows)
-        x, sst = solver.solve(rhs, op=args.op, precond=sp, method=meth, b_rows=b_rows)
+        x, sst = solver.solve(rhs, op=args.op, precond=sp, method=meth)
         solve = dict(rec(sst), solve_method=['lsqr', 'cgnr'][int(sst.get('method', 0))],
-                     solve_precond=names.get(sp, sp), solve_setup_first_s=sfirst.get('setup_s', 0.0))
+                     solve_precond=names.get(sp, sp))
         if meth == 1 and sp == 4:
-            xb, sb = solver.solve(rhs, op=args.op, precond=3, method=1, b_rows=b_rows)
+            xb, sb = solver.solve(rhs, op=args.op, precond=3, method=1)
             solve['solve_block_jacobi'] = rec(sb)
             solve['solve_rel_diff_vs_block_jacobi'] = float(np.linalg.norm(x - xb) / np.linalg.norm(xb))
         if meth == 1 and not isinstance(solver, _Dist):   # distributed LSQR has no block-Jacobi
-            xl, sl = solver.solve(rhs, op=args.op, precond=min(args.precond, 3), method=0, b_rows=b_rows)
+            xl, sl = solver.solve(rhs, op=args.op, precond=min(args.precond, 3), method=0)
             solve['solve_lsqr'] = rec(sl)
             solve['lsqr_iters_per_s'] = solve['solve_lsqr']['solve_iters_per_s']
             solve['solve_rel_diff_vs_lsqr'] = float(np.linalg.norm(x - xl) / np.linalg.norm(xl))
@@ -400,7 +391,6 @@ def main():
                                                                      if data_rows == 'matrix-free' else 'SELL data rows'))
                        if (fs.structured if isinstance(solver, _Dist) else info.get('stencil_op') and args.op == 0)
                        else 'assembled SELL',
-                       'normal_kernel': normal_kernel,
                        'parallelism': f'y-slab rows x{world} (RCCL)' if world > 1 or args.dist else 'single'},
             'device_iter_ms': 1e3 * t_dev / args.steps,
             'hbm_gbs_iter': bytes_iter * args.steps / t_dev / 1e9,
