@@ -121,11 +121,11 @@ __global__ __launch_bounds__(BLOCK) void k_block_factor(int64_t nb, const int64_
 // up to even, so a run of blocks starts 8-byte aligned).  L L^T with a triangular L whose diagonal
 // is non-zero stays SPD whatever the rounding, so CG keeps a valid preconditioner at half the bytes.
 __global__ __launch_bounds__(BLOCK) void k_block_rinv32(int64_t nb, int npk, int npks, const double* __restrict__ Ri,
-                                                        float* __restrict__ Lf) {
+                                                        lf_t* __restrict__ Lf) {
     for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < nb * npks; q += (int64_t)gridDim.x * BLOCK) {
         const int64_t b = q / npks;
         const int e = (int)(q - b * npks);
-        Lf[q] = e < npk ? (float)Ri[b * npk + e] : 0.0f;
+        Lf[q] = e < npk ? lf_round(Ri[b * npk + e]) : lf_t(0);
     }
 }
 
@@ -219,7 +219,7 @@ void block_factor_in_place(System& S) {
     hipLaunchKernelGGL(k_block_factor, dim3(grid_for(S.nblk)), dim3(BLOCK), 0, S.stream, S.nblk, S.blk_ptr.p,
                        S.blk_kmax, S.blk_Ri.p, nd.p);
     KERNEL_CHECK();
-    const int npk = S.blk_kmax * (S.blk_kmax + 1) / 2, npks = (npk + 1) & ~1;   // CGNR's fp32 copy
+    const int npk = S.blk_kmax * (S.blk_kmax + 1) / 2, npks = lf_stride(npk);   // CGNR's copy
     if (S.blk_Lf.n != (int64_t)npks * S.nblk) S.blk_Lf.alloc((int64_t)npks * S.nblk);
     hipLaunchKernelGGL(k_block_rinv32, dim3(grid_for(S.nblk * npks)), dim3(BLOCK), 0, S.stream, S.nblk, npk, npks,
                        S.blk_Ri.p, S.blk_Lf.p);
@@ -236,11 +236,11 @@ void block_factor(System& S) {
 // Multigrid coarse levels (mg.inc): nb packed blocks (AᵀA)_bb of kmax columns in Ri -> R_b⁻¹ in
 // place, then the fp32 copy Lf (block stride npks = npk rounded up to even).  ptr: device block
 // pointers (b·kmax).  Asynchronous on `st`.
-void block_factor_packed(int64_t nb, const int64_t* ptr, int kmax, double* Ri, float* Lf,
+void block_factor_packed(int64_t nb, const int64_t* ptr, int kmax, double* Ri, lf_t* Lf,
                          unsigned long long* ndead, hipStream_t st) {
     hipLaunchKernelGGL(k_block_factor, dim3(grid_for(nb)), dim3(BLOCK), 0, st, nb, ptr, kmax, Ri, ndead);
     KERNEL_CHECK();
-    const int npk = kmax * (kmax + 1) / 2, npks = (npk + 1) & ~1;
+    const int npk = kmax * (kmax + 1) / 2, npks = lf_stride(npk);
     hipLaunchKernelGGL(k_block_rinv32, dim3(grid_for(nb * npks)), dim3(BLOCK), 0, st, nb, npk, npks, Ri, Lf);
     KERNEL_CHECK();
 }

@@ -162,6 +162,35 @@ constexpr int CG_MAXI = 16;                 // (row, dim-2) items per wave of on
 constexpr int CG_MAXT = 16;
 constexpr int CG_MAX_GRP = 49;
 constexpr int CG_NCW = 16;                  // ring staging: row-image columns per lane (a wave stages whole rows: ≤ 1024)
+// Node-block factors R_b⁻¹ as the CG update and the multigrid smoother stream them: bf16 (the
+// factor was 0.33 of the update's bytes in fp32; its products stay f64).  M⁻¹ = R̃ R̃ᵀ with R̃ the
+// rounded upper-triangular R_b⁻¹ (non-zero diagonal) is SPD whatever the rounding, so PCG keeps a
+// valid preconditioner; the stopping rule, not M, fixes x.  Packed upper, block stride
+// lf_stride(npk) = npk rounded up to a whole 8-byte word.  -DLSQ_LF_F32: the fp32 copy (A/B).
+#ifdef LSQ_LF_F32
+using lf_t = float;
+#else
+using lf_t = uint16_t;
+#endif
+constexpr int LF_PER8 = 8 / (int)sizeof(lf_t);
+inline int lf_stride(int npk) { return (npk + LF_PER8 - 1) / LF_PER8 * LF_PER8; }
+__device__ __forceinline__ float lf_val(lf_t v) {
+#ifdef LSQ_LF_F32
+    return v;
+#else
+    return __uint_as_float((uint32_t)v << 16);
+#endif
+}
+__device__ __forceinline__ lf_t lf_round(double d) {
+#ifdef LSQ_LF_F32
+    return (float)d;
+#else
+    uint32_t u = __float_as_uint((float)d);   // round to nearest even on the dropped 16 bits
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (lf_t)(u >> 16);
+#endif
+}
+
 struct CgGrid {
     int32_t shape[3], col0, node0;
     int32_t ty, nty, ntx, tile0;             // tiles of the grid: ids [tile0, tile0 + nty·ntx)
@@ -314,7 +343,7 @@ struct System {
     DBuf<int32_t> blk_cols;         // compact ids
     DBuf<int32_t> blk_full;         // full ids (stencil operator v-space)
     DBuf<double> blk_Ri;
-    DBuf<float> blk_Lf;             // R_b⁻¹ in fp32 for CGNR (packed upper, block stride npk rounded to even)
+    DBuf<lf_t> blk_Lf;              // R_b⁻¹ as CGNR streams it (lf_t, packed upper, block stride lf_stride(npk))
     DBuf<double> blk_tmp;           // structured ranks: block partial sums by column (kmax × n_full) for the halo
     bool blk_valid = false;
 
@@ -460,7 +489,7 @@ void ensure_blocks(System& S);                     // default structure if none 
 void block_factor(System& S);                      // R_b⁻¹ for the current row scale
 void block_normal(System& S);                      // (AᵀA)_bb of the system's own rows into blk_Ri
 void block_factor_in_place(System& S);             // blk_Ri: (AᵀA)_bb -> R_b⁻¹
-void block_factor_packed(int64_t nb, const int64_t* ptr, int kmax, double* Ri, float* Lf,
+void block_factor_packed(int64_t nb, const int64_t* ptr, int kmax, double* Ri, lf_t* Lf,
                          unsigned long long* ndead, hipStream_t st);   // multigrid coarse blocks
 
 // dense.hip
