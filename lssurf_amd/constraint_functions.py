@@ -12,7 +12,8 @@ from .lin_op import lin_op
 
 
 def _scaled(op, base, mask_scale, scaling_masks, keys):
-    op.expected = base * op.mask_for_ind0(mask_scale)
+    op.expected = op.mask_for_ind0(mask_scale)   # a fresh array: scaled in place (base · m, bitwise)
+    op.expected *= base
     for key in keys:
         if key in scaling_masks:
             op.expected *= op.mask_for_ind0(mask=scaling_masks[key])

@@ -27,7 +27,7 @@ from .constraint_functions import build_reference_epoch_matrix, node_column_bloc
     setup_smoothness_constraints
 from .grid_functions import setup_averaging_ops, setup_avg_mask_ops, setup_grids, setup_z0_avg, \
     validate_by_dz_mask
-from .lin_op import known_range, lin_op
+from .lin_op import known_range, lin_op, toc_range
 from ._native import NativeError
 from .assemble import describe
 from .solver import LSQSolver
@@ -270,6 +270,13 @@ def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grid
     return m0, sigma_extra, in_TSE, rs_data
 
 
+def _toc_slice(op, name):
+    """op.TOC['rows'][name] as a slice when it is one contiguous run (not materialised), else the
+    index array"""
+    kr = toc_range(op.TOC['rows'], name)
+    return slice(kr[0], kr[1] + 1) if kr is not None else _as_slice(op.TOC['rows'][name])
+
+
 def _as_slice(idx):
     """A contiguous ascending index array as a slice (no fancy-indexing copy of 73 M rows)."""
     kr = known_range(idx)
@@ -288,7 +295,7 @@ def _device_constraint_stats(system, m0, Gc, R, RMS):
     names, ranges = [], []
     for eq_type in ['d2z_dt2', 'grad2_z0', 'grad2_dzdt', 'grad2_PS']:
         if eq_type in Gc.TOC['rows']:
-            rows = _as_slice(Gc.TOC['rows'][eq_type])
+            rows = _toc_slice(Gc, eq_type)
             if not isinstance(rows, slice):
                 return False
             names.append(eq_type)
@@ -323,7 +330,7 @@ def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args,
             ru = system.solver.spmv(m0[system.keep_cols])[system.n_data:] if system is not None else Gc.toCSR().dot(m0)
         for eq_type in ['d2z_dt2', 'grad2_z0', 'grad2_dzdt', 'grad2_PS']:
             if eq_type in Gc.TOC['rows']:
-                rows = _as_slice(Gc.TOC['rows'][eq_type])
+                rows = _toc_slice(Gc, eq_type)
                 rc = (1. / Ec[rows]) * ru[rows]   # TCinv_cov.dot(ru), smooth_fit.py:324-326
                 R[eq_type] = np.sum(rc ** 2)
                 RMS[eq_type] = np.sqrt(np.mean(ru[rows] ** 2))
@@ -413,13 +420,13 @@ def smooth_fit(**kwargs):
     zero_prior = set()   # priors created here are zeros: rhs is already zero on their rows
     for op in constraint_op_list:
         if op.prior is None:
-            op.prior = np.zeros_like(op.expected)
+            op.prior = np.zeros(np.shape(op.expected))   # calloc: untouched pages (73 M rows at C4)
             zero_prior.add(op.name)
     Gc = lin_op(None, name='constraints').vstack(constraint_op_list)
     N_eq = G_data.N_eq + Gc.N_eq
     Ec = np.zeros(Gc.N_eq)
     for op in constraint_op_list:
-        Ec[_as_slice(Gc.TOC['rows'][op.name])] = op.expected
+        Ec[_toc_slice(Gc, op.name)] = op.expected
     Ed = data.sigma.ravel()
     if np.any(Ed == 0):
         raise ValueError('zero value found in data sigma')
@@ -434,7 +441,7 @@ def smooth_fit(**kwargs):
     b_rows = data.size   # rhs[b_rows:] == 0: only the data rows (and non-zero priors) cross PCIe
     for op in constraint_op_list:   # rhs[data.size:] = the concatenated priors
         if op.name not in zero_prior:
-            rows = _as_slice(Gc.TOC['rows'][op.name])
+            rows = _toc_slice(Gc, op.name)
             prior = np.ravel(op.prior)
             if isinstance(rows, slice):
                 rhs[data.size + rows.start:data.size + rows.stop] = prior
