@@ -254,7 +254,8 @@ struct CgDesc {
     int32_t n_grids, ntiles, lds_max, colmode;
     int32_t nedge, maxt3, pad[2];            // column mode: workgroups of the CG iteration's k_cg_xedge (pad[0]: <8>;
                                              // pad[1]: lanes per item of the CG iteration's pass, 1 or 8); 3-D column length
-    int32_t w8, pad2;                        // column mode: the CG iteration runs k_cg_normal_col8 (8-wave workgroups)
+    int32_t w8, rw_kt;                       // column mode: the CG iteration runs k_cg_normal_col8 (8-wave workgroups);
+                                             // the wave-strip table's dim-2 class width (rw_nc; −1 one row per t)
     int32_t rw, rw_nwg;                      // the wave-strip operator k_cg_normal_rw applies; its workgroups
     CgGrid g[MF_MAX_GRIDS];
 };
