@@ -352,10 +352,15 @@ def main():
         # an untimed first solve: its set-up also captures and instantiates the iteration's hipGraph
         # (host work once per system and preconditioner — smooth_fit's later outer iterations
         # replay it); the timed solve's set-up is what every solve pays (factors, λ, first V-cycle)
-        _, sfirst = solver.solve(rhs, op=args.op, precond=sp, method=meth, b_rows=b_rows)
+        if os.environ.get('LSQ_BENCH_MAPS'):   # development: library load addresses for a host crash stack
+            with open('/proc/self/maps') as f, open(os.environ['LSQ_BENCH_MAPS'], 'w') as g:
+                g.write(f.read())
+        x1, sfirst = solver.solve(rhs, op=args.op, precond=sp, method=meth, b_rows=b_rows)
         x, sst = solver.solve(rhs, op=args.op, precond=sp, method=meth, b_rows=b_rows)
         solve = dict(rec(sst), solve_method=['lsqr', 'cgnr'][int(sst.get('method', 0))],
-                     solve_precond=names.get(sp, sp), solve_setup_first_s=sfirst.get('setup_s', 0.0))
+                     solve_precond=names.get(sp, sp), solve_setup_first_s=sfirst.get('setup_s', 0.0),
+                     solve_iters_first=int(sfirst['iters']),
+                     solve_rel_diff_first=float(np.linalg.norm(x - x1) / max(np.linalg.norm(x), 1e-300)))
         if meth == 1 and sp == 4:
             xb, sb = solver.solve(rhs, op=args.op, precond=3, method=1, b_rows=b_rows)
             solve['solve_block_jacobi'] = rec(sb)

@@ -307,6 +307,12 @@ int lsq_dgroup_iterate(lsq_dgroup* g, const double* const* b, int64_t iters, con
                        lsq_stats* s);
 const char* lsq_dgroup_last_error(lsq_dgroup* g);
 void lsq_dgroup_destroy(lsq_dgroup* g);
+/* The rank threads of a device-group call meet at a host fence before every RCCL call; a rank
+ * that fails poisons it, so the others return an error at their next collective instead of
+ * blocking in it.  Self-test of that fence (no device): n threads pass `rounds` fences, thread
+ * fail_rank (-1: none) throws before round fail_rank; returns the number of threads that left
+ * on the poisoned fence (n - 1 when one rank failed, 0 otherwise). */
+int lsq_fence_selftest(int32_t n, int32_t fail_rank, int32_t rounds);
 
 /* ---- outlier editing (RDE.py:10-18, calc_sigma_extra.py:13-44) -----
  * calc_sigma_extra's bounded search evaluates RDE(r / sqrt(s² + σ²)) 25–30 times per outer

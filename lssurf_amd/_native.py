@@ -56,7 +56,7 @@ EXPORTS = ['lsq_default_opts', 'lsq_create', 'lsq_destroy', 'lsq_last_error', 'l
            'lsq_dist_set_layout', 'lsq_dist_set_halo', 'lsq_dist_set_global', 'lsq_vgroup_create', 'lsq_vgroup_rank', 'lsq_vgroup_solve', 'lsq_vgroup_iterate',
            'lsq_vgroup_last_error', 'lsq_vgroup_destroy',
            'lsq_dgroup_create', 'lsq_dgroup_rank', 'lsq_dgroup_solve', 'lsq_dgroup_iterate', 'lsq_dgroup_last_error',
-           'lsq_dgroup_destroy',
+           'lsq_dgroup_destroy', 'lsq_fence_selftest',
            'lsq_rde_create', 'lsq_rde_order_stats', 'lsq_rde_last_error', 'lsq_rde_destroy',
            'tri_upper_solve_csr', 'tri_upper_inv_csr', 'tri_upper_rowrss_csr', 'tri_last_error']
 
@@ -123,6 +123,7 @@ def load():
         'lsq_dgroup_iterate': ([P, P, i64, P, P], ctypes.c_int),
         'lsq_dgroup_last_error': ([P], ctypes.c_char_p),
         'lsq_dgroup_destroy': ([P], None),
+        'lsq_fence_selftest': ([ctypes.c_int32, ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
         'lsq_rde_create': ([i32, i64, P, P], P),
         'lsq_rde_order_stats': ([P, f64, i64, P, P], ctypes.c_int),
         'lsq_rde_last_error': ([P], ctypes.c_char_p),

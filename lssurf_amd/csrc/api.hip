@@ -806,6 +806,7 @@ struct lsq_dgroup {
     std::vector<lsq_handle*> h;
     std::string err;
 };
+// (the rank threads of one call meet at an lsq::GroupFence before every RCCL call: dgroup_run)
 
 extern "C" {
 
@@ -863,26 +864,53 @@ static int dgroup_run(lsq_dgroup* g, lsq_stats* s, F&& f) {
     std::vector<int> rc(n, 0);
     std::vector<lsq_stats> st(n);
     std::vector<std::thread> th;
+    lsq::GroupFence fence(n);
+    std::atomic<int> first_fail{-1};
     for (int r = 0; r < n; ++r)
         th.emplace_back([&, r] {
             std::memset(&st[r], 0, sizeof(lsq_stats));
             rc[r] = guarded(g->h[r], [&](lsq::System& S) {
                 lsq::Group G;
                 G.ranks = {&S};
+                G.fence = &fence;
                 return f(G, r, &st[r]);
             });
+            // a failing rank releases the others from their next rendezvous (they fail too)
+            if (rc[r] < 0 && fence.poison()) first_fail.store(r);
         });
     for (auto& t : th) t.join();
-    for (int r = 0; r < n; ++r)
-        if (rc[r] < 0) {
-            g->err = "rank " + std::to_string(r) + ": " + g->h[r]->sys.err;
-            return rc[r];
-        }
+    if (first_fail.load() >= 0) {
+        const int r = first_fail.load();
+        g->err = "rank " + std::to_string(r) + ": " + g->h[r]->sys.err;
+        return rc[r];
+    }
     if (s) *s = st[0];
     return rc[0];
 }
 
 extern "C" {
+
+int lsq_fence_selftest(int32_t n, int32_t fail_rank, int32_t rounds) {
+    if (n < 1 || rounds < 1) return -1;
+    lsq::GroupFence fence(n);
+    std::atomic<int> left{0};
+    std::vector<std::thread> th;
+    for (int r = 0; r < n; ++r)
+        th.emplace_back([&, r] {
+            try {
+                for (int k = 0; k < rounds; ++k) {
+                    if (r == fail_rank && k == fail_rank % rounds) throw std::runtime_error("injected");
+                    fence.arrive();
+                }
+            } catch (const lsq::GroupFence::Poisoned&) {
+                left.fetch_add(1);
+            } catch (const std::exception&) {
+                fence.poison();
+            }
+        });
+    for (auto& t : th) t.join();
+    return left.load();
+}
 
 int lsq_dgroup_solve(lsq_dgroup* g, const double* const* b, double* const* x, const lsq_opts* o, lsq_stats* s) {
     if (!b || !x) return -1;

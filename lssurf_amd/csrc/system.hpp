@@ -15,7 +15,9 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/lsqsurf.h"
@@ -436,12 +438,47 @@ struct System {
 // A set of ranks solved together.  RCCL mode: the one System of this process (peers live in
 // other processes).  Virtual mode: every rank of the problem in this process, on one device and
 // one stream, exchanging by device copies — the same kernels and plans, testable on one GPU.
+// Host rendezvous of the rank threads of a device group (lsq_dgroup: one thread per device, one
+// RCCL communicator each).  Every RCCL call site passes it first, so a rank that fails before a
+// collective (an exception on that rank only: a per-rank set-up refusal, a device OOM) poisons the
+// fence and the other ranks leave with an error at their next collective instead of blocking in
+// it forever.  Spinning: the threads are dedicated to their ranks for the call.
+struct GroupFence {
+    explicit GroupFence(int n_) : n(n_) {}
+    struct Poisoned : std::runtime_error {
+        Poisoned() : std::runtime_error("another rank of the device group failed") {}
+    };
+    void arrive() {
+        if (poisoned.load(std::memory_order_acquire)) throw Poisoned();
+        const int g = gen.load(std::memory_order_acquire);
+        if (count.fetch_add(1, std::memory_order_acq_rel) + 1 == n) {
+            count.store(0, std::memory_order_relaxed);
+            gen.fetch_add(1, std::memory_order_acq_rel);
+            return;
+        }
+        while (gen.load(std::memory_order_acquire) == g) {
+            if (poisoned.load(std::memory_order_acquire)) throw Poisoned();
+            std::this_thread::yield();
+        }
+    }
+    // first caller wins: returns true for the rank whose failure is the group's
+    bool poison() { return !poisoned.exchange(true, std::memory_order_acq_rel); }
+    const int n;
+    std::atomic<int> count{0}, gen{0};
+    std::atomic<bool> poisoned{false};
+};
+
 struct Group {
     std::vector<System*> ranks;
     bool virt = false;
+    GroupFence* fence = nullptr;   // device groups: the rank threads' rendezvous before each RCCL call
     DBuf<double*> gs_ptrs;   // virtual all-reduce: device array of the ranks' gsum pointers
     DBuf<double*> vec_ptrs;  // virtual vector all-reduce: the ranks' vector pointers (scratch)
 };
+
+inline void group_fence(Group& G) {
+    if (G.fence) G.fence->arrive();
+}
 
 // dist (build.hip / lsqr.hip)
 void group_prepare_virtual(Group& G);

@@ -128,7 +128,7 @@ def window_problem(G_data, Gc, partition, rank, keep_cols):
         grids.append(d)
     pts_own = np.flatnonzero(partition.owner(py) == rank)
     rows = [pts_own]
-    local, local_fields = [], []
+    local, local_fields, part_rows = [], [], []
     row0 = pts_own.size
     for k, s in enumerate(stencils):
         gm = meta[s.grid]
@@ -144,6 +144,7 @@ def window_problem(G_data, Gc, partition, rank, keep_cols):
         k0 = (lo_y - int(s.lo[0])) * inner            # first of the part's rows kept (centre order)
         first = int(s.row0) + k0
         rows.append(first + np.arange(t.n_eq))
+        part_rows.append((row0, first, t.n_eq))       # local rows [row0, +n) = global rows [first, +n)
         if k in fields:                               # the kept rows' field values
             _, off, val, fsel, F = fields[k]
             local_fields.append((len(local), off, val, fsel, np.ascontiguousarray(F[:, k0:k0 + t.n_eq])))
@@ -177,7 +178,8 @@ def window_problem(G_data, Gc, partition, rank, keep_cols):
         glob = dict(grids=list(grid_descs), stencils=gst, local_of=np.array(local_of, np.int32), wa=wa, oa=a, ob=b,
                     rows=ny, n_full=int(max(int(g.col_0) + int(g.N_nodes) for g in order)))
     return dict(grids=grids, grid_objs=order, interp=interp, coords=coords, stencils=local, fields=local_fields,
-                npts=int(pts_own.size), rows=np.concatenate(rows), m=int(row0), n_full=int(nloc), keep=keep_local, l2g=l2g,
+                npts=int(pts_own.size), rows=np.concatenate(rows), part_rows=part_rows, m=int(row0), n_full=int(nloc),
+                keep=keep_local, l2g=l2g,
                 keep_global=pos[keep_local], own_ranges=own_ranges, meta=meta, halo=halo, glob=glob)
 
 
@@ -589,12 +591,61 @@ class VirtualDistFitSystem(_Base):
             out[prob['rows'][:prob['npts']]] = y
         return out
 
-    def solve(self, row_weight, rhs, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, method=0):
+    def rows_sumsq(self, x, ranges):
+        """lsq_rows_sumsq over the ranks: for each (first, count) range of GLOBAL rows, (Σ (w·G x)²,
+        Σ (G x)²) — each stencil row lives on the rank that owns its centre, so the per-rank sums
+        over the pieces of the range a rank holds add up to the single-GPU sums.  x: global compact.
+        Stencil rows only (data rows: data_forward)."""
+        if not self.structured:
+            raise NotImplementedError('rows_sumsq over ranks needs structured ranks')
+        sw, su = np.zeros(len(ranges)), np.zeros(len(ranges))
+        for r, prob in enumerate(self.probs):
+            pieces, which = [], []
+            for i, (g0, cnt) in enumerate(ranges):
+                for lrow0, first, n in prob['part_rows']:
+                    a, b = max(g0, first), min(g0 + cnt, first + n)
+                    if a < b:
+                        pieces.append((lrow0 + a - first, b - a))
+                        which.append(i)
+            if not pieces:
+                continue
+            h = self._rank(r)
+            xl = as_c(np.asarray(x)[prob['keep_global']], np.float64)
+            f = as_c([p_[0] for p_ in pieces], np.int64)
+            c = as_c([p_[1] for p_ in pieces], np.int64)
+            a, b = np.zeros(len(pieces)), np.zeros(len(pieces))
+            _HandleView(self.L, h).check(self.L.lsq_rows_sumsq(h, ptr(xl), len(pieces), ptr(f), ptr(c), ptr(a), ptr(b)),
+                                         'lsq_rows_sumsq')
+            np.add.at(sw, which, a)
+            np.add.at(su, which, b)
+        return sw, su
+
+    def data_colsum(self, f, n_full):
+        """G_dataᵀ f over the global full column space (f per global data row): every rank's
+        node gather over its own points, summed into the global columns of its window."""
+        out = np.zeros(int(n_full))
+        f = np.asarray(f, np.float64)
+        for r, prob in enumerate(self.probs):
+            h = self._rank(r)
+            fl = as_c(f[prob['rows'][:prob['npts']]], np.float64)
+            loc = np.zeros(prob['n_full'])
+            _HandleView(self.L, h).check(self.L.lsq_data_colsum(h, ptr(fl), ptr(loc)), 'lsq_data_colsum')
+            out[prob['l2g']] += loc
+        return out
+
+    def solve(self, row_weight, rhs, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, method=0, x0=None):
+        """x0 (global compact, CGNR on structured ranks): warm start; each rank starts from x0 on
+        its window's columns."""
         bs = self._bs(row_weight, rhs)
-        xs = [np.zeros(k) for k in self.nx]
+        warm = x0 is not None and self.structured and int(method) == 1
+        if warm:
+            xs = [np.ascontiguousarray(np.asarray(x0, np.float64)[p['keep_global']]) for p in self.probs]
+        else:
+            xs = [np.zeros(k) for k in self.nx]
         bp = (ctypes.c_void_p * self.nranks)(*[b.ctypes.data for b in bs])
         xp = (ctypes.c_void_p * self.nranks)(*[x.ctypes.data for x in xs])
-        o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond), method=int(method))
+        o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond), method=int(method),
+                         use_x0=int(warm))
         st = LsqStats()
         self._check(self._fn('solve')(self.g, bp, xp, ctypes.byref(o), ctypes.byref(st)), f'{self._api}_solve')
         self.stats = st.as_dict()
@@ -624,8 +675,10 @@ class VirtualDistFitSystem(_Base):
 class MultiDeviceFitSystem:
     """smooth_fit's device system over several GPUs of this process (smooth_fit(n_gpus=N)): the
     y-slab ranks of a device group (distinct devices) or, for testing on one GPU, a virtual group.
-    The FitSystem surface iterate_fit uses: solve with re-weighting and row editing, expand,
-    data_forward.  Warm starts are not used (every solve starts from x = 0)."""
+    The FitSystem surface iterate_fit and parse_model use: solve with re-weighting, row editing
+    and warm starts (CGNR), expand, data_forward, rows_sumsq, data_colsum — every product on the
+    ranks' devices, so no host copy of the constraint operator is made.  compute_E forms its own
+    single-device system (errors.py).
     formation = 'stencil'
     dense_ok = False        # no single-GPU dense factor over ranks
 
@@ -664,8 +717,8 @@ class MultiDeviceFitSystem:
             rhs = None                         # the ranks keep their slices
         else:
             self._rhs_last = rhs
-        x = self.group.solve(None, rhs, **{k: v for k, v in opts.items() if k in ('atol', 'btol', 'conlim', 'maxit',
-                                                                                    'precond', 'method')})
+        x = self.group.solve(None, rhs, x0=x0, **{k: v for k, v in opts.items()
+                                                   if k in ('atol', 'btol', 'conlim', 'maxit', 'precond', 'method')})
         self.stats = self.group.stats
         return x
 
@@ -676,6 +729,12 @@ class MultiDeviceFitSystem:
 
     def data_forward(self, x):
         return self.group.data_forward(x, self.n_data)
+
+    def rows_sumsq(self, x, ranges):
+        return self.group.rows_sumsq(x, ranges)
+
+    def data_colsum(self, f):
+        return self.group.data_colsum(f, self.n_full)
 
     def close(self):
         self.group.close()

@@ -122,6 +122,14 @@ class FitSystem:
         """G_data · (Ip_c x), bit-identical to scipy's csr matvec of the reference."""
         return self.solver.spmv_rows(x, 0, self.n_data)
 
+    def rows_sumsq(self, x, ranges):
+        """Per (first, count) row range of [G_data; Gc]: (Σ (w·G x)², Σ (G x)²), x compact."""
+        return self.solver.rows_sumsq(x, ranges)
+
+    def data_colsum(self, f):
+        """G_dataᵀ f over the full column space (f per data row)."""
+        return self.solver.data_colsum(f)
+
     def close(self):
         self.solver.close()
 
@@ -209,6 +217,7 @@ def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grid
         m0 = system.expand(x)
         timing['sparseqr_solve'] = time() - tic
         timing['lsq_iters'] += int(system.stats['iters'])
+        timing.setdefault('lsq_iters_per_solve', []).append(int(system.stats['iters']))
         timing['lsq_setup'] = timing.get('lsq_setup', 0.) + float(system.stats.get('setup_s', 0.))
         timing['lsq_last'] = dict(system.stats)
         tic = time()
@@ -301,7 +310,7 @@ def _device_constraint_stats(system, m0, Gc, R, RMS):
             names.append(eq_type)
             ranges.append((system.n_data + rows.start, rows.stop - rows.start))
     if names:
-        sw, su = system.solver.rows_sumsq(m0[system.keep_cols], ranges)
+        sw, su = system.rows_sumsq(m0[system.keep_cols], ranges)
         for name, (first, count), a, b in zip(names, ranges, sw, su):
             R[name] = a
             RMS[name] = np.sqrt(b / count)
@@ -327,7 +336,8 @@ def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args,
     m['jitter_bias_grids'] = {}
     if system is None or not _device_constraint_stats(system, m0, Gc, R, RMS):
         if ru is None:           # unscaled constraint residuals Gc·m0 (device product when available)
-            ru = system.solver.spmv(m0[system.keep_cols])[system.n_data:] if system is not None else Gc.toCSR().dot(m0)
+            ru = system.solver.spmv(m0[system.keep_cols])[system.n_data:] if hasattr(system, 'solver') \
+                else Gc.toCSR().dot(m0)
         for eq_type in ['d2z_dt2', 'grad2_z0', 'grad2_dzdt', 'grad2_PS']:
             if eq_type in Gc.TOC['rows']:
                 rows = _toc_slice(Gc, eq_type)
@@ -341,17 +351,22 @@ def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args,
     else:
         r_scaled = r / data.sigma[tse]
     # Gselᵀ·{1, r_scaled², r²} of smooth_fit.py:341-347: weighted column sums over the kept data rows
+    per_point = {'scaled': r_scaled ** 2, 'plain': r ** 2}
+    if 'tide' in data.fields:   # smooth_fit.py:346-352: the residual with the tide correction undone
+        r_notide = (data.z + data.tide - data.z_est)[tse]
+        per_point['notide_plain'] = r_notide ** 2
+        per_point['notide_scaled'] = (r_notide / data.sigma[tse]) ** 2
     tse_b = np.asarray(tse).astype(bool).ravel()
     n_cols = G_data.col_N
     sums = None
     if system is not None and getattr(system, 'formation', None) == 'stencil':
         fs = {'count': tse_b.astype(float)}
-        for key, vals in (('scaled', r_scaled ** 2), ('plain', r ** 2)):
+        for key, vals in per_point.items():
             f = np.zeros(tse_b.size)
             f[tse_b] = vals
             fs[key] = f
         try:   # node gather over the points sorted by cell (no host triplets of the data operator)
-            sums = {k: system.solver.data_colsum(f)[:n_cols] for k, f in fs.items()}
+            sums = {k: system.data_colsum(f)[:n_cols] for k, f in fs.items()}
         except NativeError:
             sums = None
     if sums is None:   # host: weighted column sums of G_data's triplets
@@ -361,15 +376,20 @@ def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args,
         pos[rows_tse] = np.arange(rows_tse.size)
         sel = tse_b[rr] & (vv != 0)
         c_sel, v_sel, p_sel = cc[sel], vv[sel], pos[rr[sel]]
-        sums = {'count': np.bincount(c_sel, weights=v_sel, minlength=n_cols),
-                'scaled': np.bincount(c_sel, weights=v_sel * (r_scaled ** 2)[p_sel], minlength=n_cols),
-                'plain': np.bincount(c_sel, weights=v_sel * (r ** 2)[p_sel], minlength=n_cols)}
+        sums = {'count': np.bincount(c_sel, weights=v_sel, minlength=n_cols)}
+        for key, vals in per_point.items():
+            sums[key] = np.bincount(c_sel, weights=v_sel * vals[p_sel], minlength=n_cols)
     for ff in ['dz', 'z0']:
         cols = G_data.TOC['cols'][ff]
-        m[ff].assign({'count': sums['count'][cols].reshape(grids[ff].shape)})
+        shape = grids[ff].shape
+        m[ff].assign({'count': sums['count'][cols].reshape(shape)})
         m[ff].count[m[ff].count == 0] = np.nan
-        m[ff].assign({'misfit_scaled_rms': np.sqrt(sums['scaled'][cols].reshape(grids[ff].shape) / m[ff].count)})
-        m[ff].assign({'misfit_rms': np.sqrt(sums['plain'][cols].reshape(grids[ff].shape) / m[ff].count)})
+        m[ff].assign({'misfit_scaled_rms': np.sqrt(sums['scaled'][cols].reshape(shape) / m[ff].count)})
+        m[ff].assign({'misfit_rms': np.sqrt(sums['plain'][cols].reshape(shape) / m[ff].count)})
+        if 'notide_plain' in sums:
+            m[ff].assign({'misfit_notide_rms': np.sqrt(sums['notide_plain'][cols].reshape(shape) / m[ff].count)})
+            m[ff].assign({'misfit_notide_scaled_rms':
+                          np.sqrt(sums['notide_scaled'][cols].reshape(shape) / m[ff].count)})
 
 
 def smooth_fit(**kwargs):
@@ -488,8 +508,7 @@ def smooth_fit(**kwargs):
             averaging_ops = setup_averaging_ops(grids['dz'], grids['dz'].col_N, args, grids['dz'].cell_area)
             averaging_ops.update(setup_z0_avg(grids, grids['dz'].col_N, args))
             averaging_ops.update(setup_avg_mask_ops(grids['dz'], G_data.col_N, args['avg_masks'], args['dzdt_lags']))
-            parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args,
-                        system=system if isinstance(system, FitSystem) else None)
+            parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args, system=system)
             tse = data.three_sigma_edit == 1
             r_data = data.z_est[tse] - data.z[tse]
             R['data'] = np.sum((r_data / data.sigma[tse]) ** 2)

@@ -126,9 +126,10 @@ def run_sf(LS, stubs, name, data_dict, sf_kwargs, n_outliers=0, rng=None, extra=
     for k in m:
         if k.startswith('dzdt_lag'):
             out['m_' + k] = getattr(m[k], k)
-    for f in ['count', 'misfit_rms', 'misfit_scaled_rms']:
-        out['z0_' + f] = getattr(m['z0'], f)
-        out['dz_' + f] = getattr(m['dz'], f)
+    for f in ['count', 'misfit_rms', 'misfit_scaled_rms', 'misfit_notide_rms', 'misfit_notide_scaled_rms']:
+        if hasattr(m['z0'], f):   # the notide maps exist when the data carry 'tide' (smooth_fit.py:346-352)
+            out['z0_' + f] = getattr(m['z0'], f)
+            out['dz_' + f] = getattr(m['dz'], f)
     skip = {'z0', 'dz', 'all', 'extent', 'sensor_bias_grids', 'jitter_bias_grids'}
     for k in m:
         if k not in skip and not k.startswith('dzdt_lag'):     # averaging products
@@ -201,6 +202,21 @@ def gen_eq_edit(LS, stubs):
     run_sf(LS, stubs, 'sf3d_eq_edit', {'x': x, 'y': y, 'time': t, 'z': z, 'sigma': np.full(x.size, 0.1)},
            dict(W=W, ctr=ctr, spacing={'z0': 100., 'dz': 100., 'dt': 0.25}, E_RMS=E_RMS_NB,
                 reference_epoch=3, max_iterations=3, VERBOSE=False, dzdt_lags=[1]))
+
+
+def gen_tide(LS, stubs):
+    """Data carrying a 'tide' field (parse_model's misfit_notide maps, smooth_fit.py:346-352),
+    with outliers and editing so the maps see an edited subset, and sigma_extra_relax."""
+    rng = np.random.default_rng(20251124)
+    W = {'x': 1200., 'y': 1000., 't': 1.25}
+    ctr = {'x': 0., 'y': 0., 't': 0.}
+    x, y, t, z = synth_points(rng, W, ctr, 800)
+    bad = rng.random(x.size) > 0.9
+    z[bad] += (rng.random(bad.sum()) - 0.5) * 40
+    tide = 0.3 * np.sin(2 * np.pi * t / 0.5) + rng.normal(0, 0.05, x.size)
+    run_sf(LS, stubs, 'tide', {'x': x, 'y': y, 'time': t, 'z': z, 'sigma': np.full(x.size, 0.1), 'tide': tide},
+           dict(W=W, ctr=ctr, spacing={'z0': 100., 'dz': 100., 'dt': 0.25}, E_RMS=E_RMS_NB,
+                reference_epoch=2, max_iterations=3, VERBOSE=False, dzdt_lags=[1], sigma_extra_relax=True))
 
 
 def gen_avg(LS, stubs):
@@ -461,7 +477,7 @@ def main():
     gens = {'stencils': lambda: gen_stencils(LS), 'tri': lambda: gen_tri(LS), 'lin2d': lambda: gen_lin2d(LS),
             'systems': lambda: gen_systems(LS, _refstubs), 'avg': lambda: gen_avg(LS, _refstubs),
             'kat': lambda: gen_kat(LS), 'aniso': lambda: gen_aniso(LS, _refstubs),
-            'eq_edit': lambda: gen_eq_edit(LS, _refstubs)}
+            'eq_edit': lambda: gen_eq_edit(LS, _refstubs), 'tide': lambda: gen_tide(LS, _refstubs)}
     for name in (sys.argv[1:] or list(gens)):   # e.g. `gen_golden.py aniso`: only those fixtures
         gens[name]()
 

@@ -5,6 +5,8 @@ import glob
 import os
 import re
 
+import pytest
+
 from conftest import ROOT
 
 
@@ -53,3 +55,16 @@ def test_no_gpu_create_fails_loudly():
     with pytest.raises(_native.NativeError):
         LSQSolver(0)
     assert lib is not None and n.value == 0
+
+
+@pytest.mark.timeout(60)
+def test_device_group_fence_releases_ranks_on_failure():
+    """The host fence the device group's rank threads meet at before every RCCL call (api.hip
+    dgroup_run): no failure → every thread passes every round; one rank failing before a round →
+    the other n − 1 leave with an error instead of waiting for it (no device involved)."""
+    from lssurf_amd._native import load
+    L = load()
+    assert L.lsq_fence_selftest(4, -1, 50) == 0
+    for fail in (0, 1, 3):
+        assert L.lsq_fence_selftest(4, fail, 7) == 3
+    assert L.lsq_fence_selftest(1, 0, 3) == 0

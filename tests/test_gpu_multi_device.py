@@ -101,3 +101,42 @@ def test_multi_device_row_editing(gpu_available):
     finally:
         md.close()
     assert np.linalg.norm(xd - x1) / np.linalg.norm(x1) <= 1e-8
+
+
+def test_smooth_fit_two_ranks_warm_start_and_device_outputs(gpu_available, monkeypatch):
+    """smooth_fit(n_gpus=2) on the equal-spacing editing golden (3 outer iterations, outliers):
+    the reference's edits and outputs; later outer solves warm-start from the previous solution
+    (fewer CGNR iterations than the first); parse_model's constraint R / RMS and count / misfit maps
+    come from the ranks' devices — the constraint operator is never converted to a host CSR
+    (smooth_fit.py:324-345 on the host)."""
+    from lssurf_amd import lin_op as lo
+    calls = []
+    orig = lo.lin_op.toCSR
+
+    def spy(self, *a, **k):
+        calls.append(self.name)
+        return orig(self, *a, **k)
+
+    monkeypatch.setattr(lo.lin_op, 'toCSR', spy)
+    g = golden('sys_sf3d_eq_edit.npz')
+    S = LS.smooth_fit(data=golden_points(g), n_gpus=2, devices=[0, 0], lsq_precond=3, **golden_kwargs(g))
+    assert 'constraints' not in calls, calls
+    its = S['timing']['lsq_iters_per_solve']
+    assert len(its) >= 2 and max(its[1:]) < its[0], its
+    flips = np.sum(S['data'].three_sigma_edit != g['data_three_sigma_edit'].astype(bool))
+    assert flips <= 2
+    if flips == 0:
+        assert _rel(S['m']['z0'].z0, g['z0']) < 1e-6
+        assert _rel(S['m']['dz'].dz, g['dz']) < 1e-6
+        assert _rel(S['data'].sigma_extra, g['data_sigma_extra']) < 1e-5
+        assert _rel(S['data'].z_est, g['data_z_est']) < 1e-6
+        for ff in ('z0', 'dz'):
+            for f in ('count', 'misfit_rms', 'misfit_scaled_rms'):
+                a, b = getattr(S['m'][ff], f), g[f'{ff}_{f}']
+                np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+                assert _rel(a, b) < 1e-5, (ff, f)
+        for k in g.files:
+            if k.startswith('R_') or k.startswith('RMS_'):
+                key = k.split('_', 1)[1]
+                store = S['R'] if k.startswith('R_') else S['RMS']
+                assert abs(store[key] - float(g[k])) <= 1e-5 * max(abs(float(g[k])), 1e-12), k

@@ -176,3 +176,19 @@ def test_parse_model_device_path_equals_host_path(gpu_available, name):
             np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
             ok = np.isfinite(b)
             np.testing.assert_allclose(a[ok], b[ok], rtol=1e-12, atol=0)
+
+
+def test_tide_misfit_maps(gpu_available):
+    """Data carrying 'tide': parse_model's misfit_notide_rms / misfit_notide_scaled_rms maps
+    (smooth_fit.py:346-352) next to the count / misfit maps, after 3 outer iterations of editing
+    with sigma_extra_relax, vs the reference's outputs."""
+    g = golden('sys_tide.npz')
+    S = LS.smooth_fit(data=golden_points(g), **golden_kwargs(g))
+    flips = np.sum(S['data'].three_sigma_edit != g['data_three_sigma_edit'].astype(bool))
+    assert flips == 0
+    for ff in ('z0', 'dz'):
+        for f in ('count', 'misfit_rms', 'misfit_scaled_rms', 'misfit_notide_rms', 'misfit_notide_scaled_rms'):
+            a, b = getattr(S['m'][ff], f), g[f'{ff}_{f}']
+            assert a.shape == b.shape, (ff, f)
+            np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+            assert _rel(a, b) < 1e-5, (ff, f)
