@@ -236,6 +236,7 @@ int lsq_set_row_mask(lsq_handle* h, const uint8_t* keep) {
 int lsq_shape(lsq_handle* h, int64_t* m, int64_t* n, int64_t* nnz) {
     return guarded(h, [&](lsq::System& S) {
         if (!S.G.rp.p) return fail(S, "lsq_shape: no matrix");
+        lsq::ensure_full_csr(S);
         std::vector<int64_t> rp(S.G.m + 1);
         std::vector<uint8_t> keep(S.G.m);
         S.G.rp.download(rp.data(), S.G.m + 1, S.stream);
@@ -254,6 +255,7 @@ int lsq_shape(lsq_handle* h, int64_t* m, int64_t* n, int64_t* nnz) {
 int lsq_get_csr(lsq_handle* h, int64_t* indptr, int32_t* indices, double* data) {
     return guarded(h, [&](lsq::System& S) {
         if (!S.G.rp.p) return fail(S, "lsq_get_csr: no matrix");
+        lsq::ensure_full_csr(S);
         const int64_t m = S.G.m, z = S.G.nnz;
         std::vector<int64_t> rp(m + 1);
         std::vector<int32_t> ci(std::max<int64_t>(z, 1));
@@ -404,7 +406,7 @@ int lsq_sell_info(lsq_handle* h, int64_t* out8) {
         if (!out8) return fail(S, "lsq_sell_info: null output");
         out8[0] = S.G.m;
         out8[1] = S.G.n;
-        out8[2] = S.G.nnz;
+        out8[2] = S.g_full ? S.G.nnz : S.nnz_full;   // the formed operator's nnz
         out8[3] = S.mf ? S.Ad.nent : S.A.nent;
         out8[4] = S.mf ? S.ATd.nnz : S.AT.nent;
         out8[5] = (int64_t)(S.G.rp.bytes() + S.G.ci.bytes() + S.G.val.bytes() + S.GT.rp.bytes() + S.GT.ci.bytes() +

@@ -50,8 +50,7 @@ __global__ __launch_bounds__(BLOCK) void k_gen_rows(int pass, const GenCtx* __re
                                                     const double* __restrict__ pt, const int32_t* __restrict__ colmap,
                                                     int64_t* __restrict__ cnt, const int64_t* __restrict__ rp,
                                                     int32_t* __restrict__ ci, double* __restrict__ val,
-                                                    unsigned long long* __restrict__ err) {
-    const int64_t m = ctx->m;
+                                                    unsigned long long* __restrict__ err, int64_t m) {
     for (int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x; r < m; r += (int64_t)gridDim.x * BLOCK) {
         int64_t cols[MAXE];
         double vals[MAXE];
@@ -345,6 +344,53 @@ void describe_global(System& S, int64_t n_full, int32_t n_grids, const lsq_grid_
     S.dg_mfh = d;
 }
 
+namespace {
+
+// G's row pointers for all m rows (count pass: validates every row and gives the formed nnz), then
+// the entries of the first `rows` rows (fill pass).  S.G.m = m either way; rows < m keeps npts + 1
+// row pointers (the lazy structured formation: rows = the data rows).
+void gen_rows_csr(System& S, const double* dy, const double* dx, const double* dt, int64_t rows) {
+    hipStream_t strm = S.stream;
+    const GenCtx& h = *reinterpret_cast<const GenCtx*>(S.gen_ctx.data());
+    const int64_t m = h.m;
+    DBuf<GenCtx> dctx(1);
+    HIP_CHECK(hipMemcpyAsync(dctx.p, &h, sizeof(GenCtx), hipMemcpyHostToDevice, strm));
+    DBuf<unsigned long long> err(1);
+    err.zero(strm);
+    const int32_t* cmap = S.have_colmap ? S.colmap.p : nullptr;
+    DBuf<int64_t> rp(m + 1);
+    rp.zero(strm);
+    hipLaunchKernelGGL(k_gen_rows, dim3(grid_for(m)), dim3(BLOCK), 0, strm, 0, dctx.p, dy, dx, dt, cmap, rp.p, nullptr,
+                       nullptr, nullptr, err.p, m);
+    KERNEL_CHECK();
+    S.nnz_full = exclusive_scan_i64(rp.p, m + 1, strm);
+    Csr& G = S.G;
+    G.m = m;
+    G.n = S.have_colmap ? S.n_keep : h.n_full;
+    if (rows < m) {
+        G.rp.alloc(rows + 1);
+        HIP_CHECK(hipMemcpyAsync(G.rp.p, rp.p, sizeof(int64_t) * (rows + 1), hipMemcpyDeviceToDevice, strm));
+        HIP_CHECK(hipMemcpyAsync(&G.nnz, rp.p + rows, sizeof(int64_t), hipMemcpyDeviceToHost, strm));
+        HIP_CHECK(hipStreamSynchronize(strm));   // rp is released below
+    } else {
+        G.rp = std::move(rp);
+        G.nnz = S.nnz_full;
+    }
+    G.ci.alloc(std::max<int64_t>(G.nnz, 1));
+    G.val.alloc(std::max<int64_t>(G.nnz, 1));
+    if (rows > 0)
+        hipLaunchKernelGGL(k_gen_rows, dim3(grid_for(rows)), dim3(BLOCK), 0, strm, 1, dctx.p, dy, dx, dt, cmap, nullptr,
+                           G.rp.p, G.ci.p, G.val.p, err.p, rows);
+    KERNEL_CHECK();
+    unsigned long long herr = 0;
+    HIP_CHECK(hipMemcpyAsync(&herr, err.p, sizeof(herr), hipMemcpyDeviceToHost, strm));
+    HIP_CHECK(hipStreamSynchronize(strm));
+    if (herr) throw std::invalid_argument("lsq_set_matrix_stencil: " + std::to_string(herr) +
+                                          " nonzero entries fall outside [0, n_full)");
+}
+
+}  // namespace
+
 void form_from_stencils(System& S, int64_t m, int64_t n_full, int32_t n_grids, const lsq_grid_desc* grids,
                         int32_t n_interp, const int32_t* interp_grid, int64_t npts, const double* py,
                         const double* px, const double* pt, int32_t n_stencil, const lsq_stencil_desc* st) {
@@ -419,9 +465,15 @@ void form_from_stencils(System& S, int64_t m, int64_t n_full, int32_t n_grids, c
     if (npts > 0 && (!py || !px || (need_t && !pt))) throw std::invalid_argument("missing point coordinates");
 
     hipStream_t strm = S.stream;
-    const int64_t n = S.have_colmap ? S.n_keep : n_full;
-    DBuf<GenCtx> dctx(1);
-    HIP_CHECK(hipMemcpyAsync(dctx.p, &h, sizeof(GenCtx), hipMemcpyHostToDevice, strm));
+    S.n_sorted_rows = npts;   // data rows: point order is random in space
+    S.mf = !S.dist && describe_stencil_operator(S.mfh, m, n_full, n_grids, grids, npts, n_stencil, h.st);
+    if (S.has_var && !S.mf)
+        throw std::invalid_argument("lsq_set_matrix_stencil: field-valued parts need the structured operator "
+                                    "(single GPU, parts inside their grids, |offsets| <= 3)");
+    // structured single-GPU systems store only the data rows (System::g_full; LSQ_FULL_CSR=1 forms
+    // everything up front, for A/B)
+    static const bool full_env = getenv("LSQ_FULL_CSR") && getenv("LSQ_FULL_CSR")[0] == '1';
+    const bool lazy = S.mf && !full_env;
     DBuf<double> dy(std::max<int64_t>(npts, 1)), dx(std::max<int64_t>(npts, 1)), dt;
     dy.upload(py, npts, strm);
     dx.upload(px, npts, strm);
@@ -429,37 +481,35 @@ void form_from_stencils(System& S, int64_t m, int64_t n_full, int32_t n_grids, c
         dt.alloc(std::max<int64_t>(npts, 1));
         dt.upload(pt, npts, strm);
     }
-    DBuf<unsigned long long> err(1);
-    err.zero(strm);
-    Csr& G = S.G;
-    G.m = m;
-    G.n = n;
-    G.rp.alloc(m + 1);
-    G.rp.zero(strm);
-    const int32_t* cmap = S.have_colmap ? S.colmap.p : nullptr;
-    const int grid = grid_for(m);
-    hipLaunchKernelGGL(k_gen_rows, dim3(grid), dim3(BLOCK), 0, strm, 0, dctx.p, dy.p, dx.p, dt.p, cmap, G.rp.p,
-                       nullptr, nullptr, nullptr, err.p);
-    KERNEL_CHECK();
-    G.nnz = exclusive_scan_i64(G.rp.p, m + 1, strm);
-    G.ci.alloc(std::max<int64_t>(G.nnz, 1));
-    G.val.alloc(std::max<int64_t>(G.nnz, 1));
-    hipLaunchKernelGGL(k_gen_rows, dim3(grid), dim3(BLOCK), 0, strm, 1, dctx.p, dy.p, dx.p, dt.p, cmap, nullptr,
-                       G.rp.p, G.ci.p, G.val.p, err.p);
-    KERNEL_CHECK();
-    unsigned long long herr = 0;
-    HIP_CHECK(hipMemcpyAsync(&herr, err.p, sizeof(herr), hipMemcpyDeviceToHost, strm));
-    HIP_CHECK(hipStreamSynchronize(strm));
-    if (herr) throw std::invalid_argument("lsq_set_matrix_stencil: " + std::to_string(herr) +
-                                          " nonzero entries fall outside [0, n_full)");
-    S.n_sorted_rows = npts;   // data rows: point order is random in space
-    S.mf = !S.dist && describe_stencil_operator(S.mfh, m, n_full, n_grids, grids, npts, n_stencil, h.st);
-    if (S.has_var && !S.mf)
-        throw std::invalid_argument("lsq_set_matrix_stencil: field-valued parts need the structured operator "
-                                    "(single GPU, parts inside their grids, |offsets| <= 3)");
+    S.G = Csr{};
+    S.GT = Csr{};
+    S.gen_ctx.assign(reinterpret_cast<const char*>(&h), reinterpret_cast<const char*>(&h) + sizeof(GenCtx));
+    S.g_full = true;
+    gen_rows_csr(S, dy.p, dx.p, need_t ? dt.p : nullptr, lazy ? npts : m);
+    if (lazy) {   // kept for ensure_full_csr
+        S.gen_py = std::move(dy);
+        S.gen_px = std::move(dx);
+        S.gen_pt = std::move(dt);
+        S.g_full = false;
+    } else {
+        S.gen_ctx.clear();
+    }
     finish_formation(S);
     if (S.mf) build_dmf(S, n_grids, grids, n_interp, interp_grid, npts, py, px, pt);
 }
+
+void ensure_full_csr(System& S) {
+    if (S.g_full) return;
+    gen_rows_csr(S, S.gen_py.p, S.gen_px.p, S.gen_pt.n ? S.gen_pt.p : nullptr, S.G.m);
+    S.g_full = true;
+    S.gen_py = DBuf<double>();
+    S.gen_px = DBuf<double>();
+    S.gen_pt = DBuf<double>();
+    S.gen_ctx.clear();
+    full_transpose(S);
+}
+
+int64_t stored_rows(const System& S) { return S.g_full ? S.G.m : S.mfh.npts; }
 
 // z0 (gz) on a 2× refinement of the dz (g3) lattice: the points sorted by dz cell with their dz
 // subscripts — the data rows of the system Galerkin-projected onto the dz lattice (z0's bilinear

@@ -763,6 +763,7 @@ void run_sweeps(hipStream_t st, const BandDev& b, int64_t nwg, int64_t cap, cons
 // nw ≥ 0: the first nw entries of h_perm are a WINDOW of the columns; the factor is that of the
 // principal submatrix (AᵀA)_WW = A_WᵀA_W (every other column held fixed)
 void band_factor(System& S, const int32_t* h_perm, BandFactor& F, int64_t nw) {
+    ensure_full_csr(S);   // the band of AᵀA from G / GT
     hipStream_t st = S.stream;
     const int64_t ncol = S.G.n;
     const int64_t n = nw >= 0 ? nw : ncol;

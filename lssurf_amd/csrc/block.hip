@@ -67,6 +67,76 @@ __global__ __launch_bounds__(BLOCK) void k_block_normal(int64_t nb, int kmax, co
     }
 }
 
+// (AᵀA)_bb of a lazily formed structured system (System::g_full = false: no GT): the data rows by
+// the merge over GdT (their transpose, rows = compact columns) and the stencil rows from the part
+// descriptors — for columns i, j of one grid, Σ over the parts' rows that hold both: a row of
+// centre c = sub(i) − off_t holds j when c + off_t2 = sub(j).  Same products as the GT merge.
+__global__ __launch_bounds__(BLOCK) void k_block_normal_mf(int64_t nb, int kmax, const int64_t* __restrict__ ptr,
+                                                           const int32_t* __restrict__ cols,
+                                                           const int32_t* __restrict__ full,
+                                                           const int64_t* __restrict__ trp,
+                                                           const int32_t* __restrict__ tci,
+                                                           const double* __restrict__ tval,
+                                                           const MfDesc* __restrict__ dd,
+                                                           const double* __restrict__ rs, double* __restrict__ N) {
+    const MfDesc& d = *dd;
+    const int npk = kmax * (kmax + 1) / 2;
+    const int64_t total = nb * npk;
+    for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < total; q += (int64_t)gridDim.x * BLOCK) {
+        const int64_t b = q / npk;
+        const int e = (int)(q - b * npk);
+        int j = 0;
+        while ((j + 1) * (j + 2) / 2 <= e) ++j;
+        const int i = e - j * (j + 1) / 2;
+        const int64_t b0 = ptr[b];
+        const int k = (int)(ptr[b + 1] - b0);
+        if (j >= k) {
+            N[q] = 0.0;
+            continue;
+        }
+        double s = col_dot(trp, tci, tval, rs, cols[b0 + i], cols[b0 + j]);
+        const int64_t fi = full[b0 + i], fj = full[b0 + j];
+        for (int g = 0; g < d.n_grids; ++g) {
+            const MfGrid& G = d.g[g];
+            if (!G.nparts || fi < G.col0 || fi >= (int64_t)G.col0 + G.nodes) continue;
+            if (fj < G.col0 || fj >= (int64_t)G.col0 + G.nodes) break;
+            const int nd = G.ndim;
+            int64_t si[3] = {0, 0, 0}, sj[3] = {0, 0, 0};
+            int64_t ri = fi - G.col0, rj = fj - G.col0;
+            for (int a = nd - 1; a >= 0; --a) {
+                si[a] = ri % G.shape[a];
+                ri /= G.shape[a];
+                sj[a] = rj % G.shape[a];
+                rj /= G.shape[a];
+            }
+            for (int pp = 0; pp < G.nparts; ++pp) {
+                const MfPart& P = d.p[G.part[pp]];
+                for (int t = 0; t < P.ntpl; ++t) {
+                    int64_t kk = 0;
+                    bool in = true;
+                    for (int a = 0; a < nd; ++a) {
+                        const int64_t c = si[a] - P.off[t][a];
+                        in = in && c >= P.lo[a] && c < P.hi[a];
+                        kk = kk * (P.hi[a] - P.lo[a]) + (c - P.lo[a]);
+                    }
+                    if (!in) continue;
+                    const double w = rs[P.row0 + kk];
+                    const double vi = P.var ? P.val[t] * P.F[(int64_t)P.fsel[t] * P.n_eq + kk] : P.val[t];
+                    for (int t2 = 0; t2 < P.ntpl; ++t2) {
+                        bool hit = true;
+                        for (int a = 0; a < nd; ++a) hit = hit && si[a] - P.off[t][a] + P.off[t2][a] == sj[a];
+                        if (!hit) continue;
+                        const double vj = P.var ? P.val[t2] * P.F[(int64_t)P.fsel[t2] * P.n_eq + kk] : P.val[t2];
+                        s += (w * vi) * (w * vj);
+                    }
+                }
+            }
+            break;
+        }
+        N[q] = s;
+    }
+}
+
 // In place: N_b -> R_b (Cholesky, upper) -> R_b⁻¹, one thread per block
 __global__ __launch_bounds__(BLOCK) void k_block_factor(int64_t nb, const int64_t* __restrict__ ptr, int kmax,
                                                         double* __restrict__ Ri, unsigned long long* ndead) {
@@ -207,8 +277,13 @@ void block_normal(System& S) {
     ensure_blocks(S);
     const int npk = S.blk_kmax * (S.blk_kmax + 1) / 2;
     if (S.blk_Ri.n != (int64_t)npk * S.nblk) S.blk_Ri.alloc((int64_t)npk * S.nblk);
-    hipLaunchKernelGGL(k_block_normal, dim3(grid_for(S.nblk * npk)), dim3(BLOCK), 0, S.stream, S.nblk, S.blk_kmax,
-                       S.blk_ptr.p, S.blk_cols.p, S.GT.rp.p, S.GT.ci.p, S.GT.val.p, S.rs.p, S.blk_Ri.p);
+    if (!S.g_full)   // lazily formed structured system: GdT + the stencil parts
+        hipLaunchKernelGGL(k_block_normal_mf, dim3(grid_for(S.nblk * npk)), dim3(BLOCK), 0, S.stream, S.nblk,
+                           S.blk_kmax, S.blk_ptr.p, S.blk_cols.p, S.blk_full.p, S.GdT.rp.p, S.GdT.ci.p, S.GdT.val.p,
+                           S.mfd.p, S.rs.p, S.blk_Ri.p);
+    else
+        hipLaunchKernelGGL(k_block_normal, dim3(grid_for(S.nblk * npk)), dim3(BLOCK), 0, S.stream, S.nblk, S.blk_kmax,
+                           S.blk_ptr.p, S.blk_cols.p, S.GT.rp.p, S.GT.ci.p, S.GT.val.p, S.rs.p, S.blk_Ri.p);
     KERNEL_CHECK();
 }
 

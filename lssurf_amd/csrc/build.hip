@@ -400,6 +400,54 @@ __global__ __launch_bounds__(BLOCK) void k_rows_sumsq(int64_t first, int64_t cou
     }
 }
 
+// Row r of stencil part P (r − P.row0 = k, the centre's position in the part's box), straight from
+// the part descriptor as k_gen_rows generates it: entry t at full column col0 + ravel(c + off_t),
+// value val_t (· F[fsel_t][k] for a field-valued part).  xf: full column space (removed columns 0).
+__device__ double mf_stencil_row(const MfDesc& d, const MfPart& P, int64_t k, const double* __restrict__ xf) {
+    const MfGrid& G = d.g[P.grid];
+    const int nd = G.ndim;
+    int64_t sub[3] = {0, 0, 0}, gst[3] = {1, 1, 1}, rem = k;
+    for (int e = nd - 1; e >= 0; --e) {
+        const int64_t ext = P.hi[e] - P.lo[e];
+        sub[e] = P.lo[e] + rem % ext;
+        rem /= ext;
+        if (e < nd - 1) gst[e] = gst[e + 1] * G.shape[e + 1];
+    }
+    double acc = 0.0;
+    for (int t = 0; t < P.ntpl; ++t) {
+        int64_t col = G.col0;
+        for (int e = 0; e < nd; ++e) col += (sub[e] + P.off[t][e]) * gst[e];
+        const double v = P.var ? P.val[t] * P.F[(int64_t)P.fsel[t] * P.n_eq + k] : P.val[t];
+        acc += v * xf[col];
+    }
+    return acc;
+}
+
+// k_rows_sumsq for rows of the stencil parts of a lazily formed system (rows ≥ npts)
+__global__ __launch_bounds__(BLOCK) void k_rows_sumsq_mf(const MfDesc* __restrict__ dd, int64_t first, int64_t count,
+                                                         const double* __restrict__ xf, const double* __restrict__ w,
+                                                         double* __restrict__ pw, double* __restrict__ pu) {
+    const MfDesc& d = *dd;
+    double aw = 0.0, au = 0.0;
+    for (int64_t r = first + (int64_t)blockIdx.x * BLOCK + threadIdx.x; r < first + count; r += (int64_t)gridDim.x * BLOCK) {
+        int p = 0;
+        while (p + 1 < d.n_parts && r >= d.p[p + 1].row0) ++p;
+        const MfPart& P = d.p[p];
+        const double acc = mf_stencil_row(d, P, r - P.row0, xf);
+        const double rc = (w ? w[r] : 1.0) * acc;
+        aw += rc * rc;
+        au += acc * acc;
+    }
+    __shared__ double red[4];
+    const double sw = block_sum(aw, red);
+    __syncthreads();
+    const double su = block_sum(au, red);
+    if (threadIdx.x == 0) {
+        pw[blockIdx.x] = sw;
+        pu[blockIdx.x] = su;
+    }
+}
+
 // distributed layout: mark referenced columns; relabel columns to local ids and re-sort rows
 __global__ __launch_bounds__(BLOCK) void k_flag_cols(int64_t nnz, const int32_t* __restrict__ ci,
                                                      uint8_t* __restrict__ flags) {
@@ -582,6 +630,7 @@ void transpose_rows(const Csr& G, int64_t rows, Csr& T, hipStream_t st) {
 // column; AT's column ids = A's SELL row ids).
 void ensure_sell(System& S) {
     if (S.sell_built) return;
+    ensure_full_csr(S);
     hipStream_t st = S.stream;
     DBuf<int32_t> inv;
     locality_order(S.G, S.G.m, S.n_sorted_rows, S.A.perm, inv, st);
@@ -681,7 +730,7 @@ void finish_formation(System& S) {
     hipStream_t st = S.stream;
     Csr& G = S.G;
     const int64_t m = G.m, n = G.n;
-    transpose_rows(G, m, S.GT, st);
+    if (S.g_full) transpose_rows(G, m, S.GT, st);   // lazy structured formation: GT with the full G
     S.sell_built = false;
     S.A = Sell();
     S.AT = Sell();
@@ -705,6 +754,11 @@ void finish_formation(System& S) {
     S.blk_user = false;
     S.blk_valid = false;
     HIP_CHECK(hipStreamSynchronize(st));
+}
+
+void full_transpose(System& S) {
+    transpose_rows(S.G, S.G.m, S.GT, S.stream);
+    HIP_CHECK(hipStreamSynchronize(S.stream));
 }
 
 // Scaling is applied in three phases so a distributed group can exchange column norms between
@@ -792,6 +846,7 @@ void refresh_scaling(System& S, int precond) {
 }
 
 void csr_spmv(System& S, int trans, const double* dx, double* dy) {
+    ensure_full_csr(S);
     const Csr& C = trans ? S.GT : S.G;
     hipLaunchKernelGGL(k_csr_spmv, dim3(grid_for(C.m)), dim3(BLOCK), 0, S.stream, C.m, C.rp.p, C.ci.p, C.val.p, dx, dy);
     KERNEL_CHECK();
@@ -799,6 +854,7 @@ void csr_spmv(System& S, int trans, const double* dx, double* dy) {
 
 void csr_spmv_rows(System& S, int64_t first, int64_t count, const double* dx, double* dy) {
     if (!count) return;
+    if (first + count > stored_rows(S)) ensure_full_csr(S);
     hipLaunchKernelGGL(k_csr_spmv, dim3(grid_for(count)), dim3(BLOCK), 0, S.stream, count, S.G.rp.p + first, S.G.ci.p,
                        S.G.val.p, dx, dy);
     KERNEL_CHECK();
@@ -807,8 +863,24 @@ void csr_spmv_rows(System& S, int64_t first, int64_t count, const double* dx, do
 void csr_rows_sumsq(System& S, const double* dx, int64_t first, int64_t count, double* h_w, double* h_u) {
     const int nb = grid_for(std::max<int64_t>(count, 1));
     DBuf<double> pw(nb), pu(nb);
-    hipLaunchKernelGGL(k_rows_sumsq, dim3(nb), dim3(BLOCK), 0, S.stream, first, count, S.G.rp.p, S.G.ci.p, S.G.val.p, dx,
-                       S.roww.p, pw.p, pu.p);
+    const int64_t ns = stored_rows(S);
+    if (first + count <= ns) {
+        hipLaunchKernelGGL(k_rows_sumsq, dim3(nb), dim3(BLOCK), 0, S.stream, first, count, S.G.rp.p, S.G.ci.p, S.G.val.p,
+                           dx, S.roww.p, pw.p, pu.p);
+    } else if (first >= ns) {   // stencil rows of a lazily formed system: from the part descriptors
+        DBuf<double> xf(std::max<int64_t>(S.n_full, 1));
+        xf.zero(S.stream);
+        hipLaunchKernelGGL(k_scatter_cs, dim3(grid_for(S.G.n)), dim3(BLOCK), 0, S.stream, S.G.n, S.keep.p, dx, xf.p);
+        hipLaunchKernelGGL(k_rows_sumsq_mf, dim3(nb), dim3(BLOCK), 0, S.stream, S.mfd.p, first, count, xf.p, S.roww.p,
+                           pw.p, pu.p);
+    } else {   // a range across the data / stencil boundary: the two pieces
+        double w1, u1, w2, u2;
+        csr_rows_sumsq(S, dx, first, ns - first, &w1, &u1);
+        csr_rows_sumsq(S, dx, ns, first + count - ns, &w2, &u2);
+        *h_w = w1 + w2;
+        *h_u = u1 + u2;
+        return;
+    }
     KERNEL_CHECK();
     std::vector<double> hw(nb), hu(nb);
     pw.download(hw.data(), nb, S.stream);
@@ -824,6 +896,7 @@ void csr_rows_sumsq(System& S, const double* dx, int64_t first, int64_t count, d
 }
 
 void referenced_cols(System& S, uint8_t* h_flags) {
+    ensure_full_csr(S);
     DBuf<uint8_t> f(std::max<int64_t>(S.G.n, 1));
     f.zero(S.stream);
     hipLaunchKernelGGL(k_flag_cols, dim3(grid_for(S.G.nnz)), dim3(BLOCK), 0, S.stream, S.G.nnz, S.G.ci.p, f.p);
@@ -833,6 +906,7 @@ void referenced_cols(System& S, uint8_t* h_flags) {
 }
 
 void relabel_columns(System& S, const int32_t* h_map, int64_t n_local) {
+    ensure_full_csr(S);
     S.dmf.ok = 0;   // the matrix-free data rows address the formation's column space
     DBuf<int32_t> map(std::max<int64_t>(S.G.n, 1));
     map.upload(h_map, S.G.n, S.stream);

@@ -297,6 +297,7 @@ __global__ __launch_bounds__(BLOCK) void k_gemvT_upper(const double* __restrict_
 
 // Build R (in place of N) and R⁻¹ for the current row scaling.  Throws if N is not SPD.
 void dense_factor(System& S) {
+    ensure_full_csr(S);   // AᵀA from GT
     hipStream_t st = S.stream;
     const int64_t n = S.G.n;
     const int64_t npad = (n + TB - 1) / TB * TB, ld = npad;

@@ -307,6 +307,16 @@ struct System {
     bool rs_dirty = true;
     Sell A, AT;
     bool sell_built = false;   // A / AT exist (built lazily when the stencil operator is active)
+    // Lazy full CSR (structured single-GPU systems): formation stores only the data rows of G
+    // (rows [0, npts): Ad, ATd and their values come from them) — the CGNR / LSQR stencil operator,
+    // the node-block factors and the constraint-row sums never read the 10⁷–10⁸ stencil rows.  G
+    // then keeps G.m = m (logical rows) with npts + 1 row pointers, nnz_full is the formed nnz, and
+    // GT is empty until ensure_full_csr() forms both from the generation context kept here (the
+    // assembled SELL operator, dense / band factors, lsq_get_csr, lsq_spmv).
+    bool g_full = true;
+    int64_t nnz_full = 0;
+    std::vector<char> gen_ctx;            // GenCtx bytes (assemble.hip)
+    DBuf<double> gen_py, gen_px, gen_pt;  // point coordinates of the data rows
 
     // field-valued stencil parts (lsq_set_stencil_fields): staged by stencil index before the
     // structured formation; the device fields live as long as the matrix (MfPart::F)
@@ -489,10 +499,15 @@ int group_cg_iterate(Group& G, const double* const* h_b, int64_t iters, const ls
 void referenced_cols(System& S, uint8_t* h_flags);
 void relabel_columns(System& S, const int32_t* h_map, int64_t n_local);
 
+// assemble.hip: the full G / GT of a lazily formed structured system (no-op when formed)
+void ensure_full_csr(System& S);
+int64_t stored_rows(const System& S);            // rows of G whose entries are stored
+
 // build.hip
 void form_from_coo(System& S, int64_t m, int64_t n_full, int64_t nnz, const int64_t* r,
                    const int64_t* c, const double* v);
 void finish_formation(System& S);              // G set -> GT, SELL copies, default scaling
+void full_transpose(System& S);                 // GT of the (full) G
 void describe_global(System& S, int64_t n_full, int32_t n_grids, const lsq_grid_desc* grids, int32_t n_stencil,
                      const lsq_stencil_desc* st);   // S.dg_mfh (lsq_dist_set_global)
 void build_dmf(System& S, int32_t n_grids, const lsq_grid_desc* grids, int32_t n_interp, const int32_t* interp_grid,

@@ -678,7 +678,7 @@ class MultiDeviceFitSystem:
     The FitSystem surface iterate_fit and parse_model use: solve with re-weighting, row editing
     and warm starts (CGNR), expand, data_forward, rows_sumsq, data_colsum — every product on the
     ranks' devices, so no host copy of the constraint operator is made.  compute_E forms its own
-    single-device system (errors.py).
+    single-device system (errors.py)."""
     formation = 'stencil'
     dense_ok = False        # no single-GPU dense factor over ranks
 
