@@ -47,15 +47,16 @@ typedef struct lsq_opts {
     int32_t method;        /* 0 = LSQR (Paige & Saunders 1982); 1 = CGNR: preconditioned CG on  */
                            /*     the normal equations with the fused normal-stencil operator   */
                            /*     (structured systems, single-GPU or structured ranks; precond  */
-                           /*     1 or 3; other single-GPU systems fall back to LSQR and report */
-                           /*     method 0 in lsq_stats)                                        */
+                           /*     1, 3 or 4; other single-GPU systems fall back to LSQR and     */
+                           /*     report method 0 in lsq_stats)                                 */
     int32_t precond;       /* 0 = none, 1 = column (Jacobi) scaling, 2 = dense Cholesky R⁻¹   */
                            /*     (exact right preconditioner; n up to a few 10^4), 3 = block-  */
                            /*     Jacobi: R_b⁻¹ of every column block (lsq_set_column_blocks;   */
                            /*     SURVEY.md §8 a7.4 — no reference counterpart), 4 = geometric  */
                            /*     multigrid V-cycle over the (y, x) node lattice (method 1,     */
-                           /*     single-GPU smooth_fit systems with per-node column blocks;    */
-                           /*     DESIGN.md §Multigrid), 5 = banded Cholesky R̃⁻¹ in the order of */
+                           /*     smooth_fit systems with per-node column blocks, single GPU or */
+                           /*     structured ranks with lsq_dist_set_global; DESIGN.md          */
+                           /*     §Multigrid), 5 = banded Cholesky R̃⁻¹ in the order of         */
                            /*     lsq_set_band_order (LSQR, single GPU; band.hip)               */
     double  atol, btol, conlim;
     int64_t maxit;

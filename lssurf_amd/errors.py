@@ -55,6 +55,9 @@ def band_order(grids, keep_cols):
 
 WINDOW_MIN_COLS = 250_000      # 'auto': the full band below, tiled windows above
 WINDOW_TILE, WINDOW_MARGIN = 64, 24   # σ within ~3e-6 of the full band at 128²×12 (tests)
+WINDOW_CHECK_TOL = 1e-4        # self-check bound: σ of a sample tile at twice the margin (the margin
+                               # doubles, up to 4×, until it holds; the reference's own Rinv
+                               # truncation moves σ by ~1e-5)
 
 
 def _node_index(grids, keep_cols):
@@ -127,10 +130,19 @@ def window_cov(solver, grids, keep_cols, op=None, tile=WINDOW_TILE, margin=WINDO
             win = (iy_o >= b[0] - margin) & (iy_o <= b[1] + margin) & (ix_o >= b[2] - margin) & (ix_o <= b[3] + margin)
             wmax = max(wmax, run(win, None, rows))
             nown += 1
+    # self-check: the most central tile again with twice the margin; σ of its columns moves by the
+    # correlations the margin cut off (conditional vs marginal variance)
+    cy, cx = (ny // 2) // tile * tile, (nx // 2) // tile * tile
+    inner = (iy >= cy) & (iy < cy + tile) & (ix >= cx) & (ix < cx + tile)
+    m2 = 2 * margin
+    win2 = (iy_o >= cy - m2) & (iy_o < cy + tile + m2) & (ix_o >= cx - m2) & (ix_o < cx + tile + m2)
+    E2, _, _ = solver.cov_band_window(order[win2], None)
+    sel = inner & (E2 > 0)
+    check = float(np.max(np.abs(E[sel] - E2[sel]) / E2[sel])) if sel.any() else 0.0
     if timing is not None:
         timing['E_window'] = {'tiles': ntiles, 'op_windows': nown, 'tile': tile, 'margin': margin,
-                              'max_band_tiles': wmax}
-    return E, op_err
+                              'max_band_tiles': wmax, 'selfcheck_rel': check, 'selfcheck_margin': m2}
+    return E, op_err, check
 
 
 def _compact_rows(op, keep_cols, n_full):
@@ -153,6 +165,7 @@ def calc_and_parse_errors(E, G_data, Gc, Ed, Ec, data, in_TSE, keep_cols, grids,
                           method='auto'):
     timing = {} if timing is None else timing
     tic = time()
+    approx = None   # window method: how σ was approximated (attached to the output grids)
     sigma_data = np.sqrt(Ed ** 2 + data.sigma_extra ** 2)
     E_all = np.concatenate((sigma_data, Ec))
     w = 1. / E_all                                   # TCinv, smooth_fit.py:697
@@ -167,8 +180,20 @@ def calc_and_parse_errors(E, G_data, Gc, Ed, Ec, data, in_TSE, keep_cols, grids,
             keys = list(avg_ops)
             mats = [_compact_rows(avg_ops[k], keep_cols, Gc.col_N) for k in keys]
             op = sp.vstack(mats).tocsr() if mats else None
-            E0c, errs = window_cov(fs.solver, grids, keep_cols, op, tile=WINDOW_TILE, margin=WINDOW_MARGIN,
-                                   timing=timing)
+            margin = WINDOW_MARGIN
+            while True:
+                E0c, errs, check = window_cov(fs.solver, grids, keep_cols, op, tile=WINDOW_TILE, margin=margin,
+                                              timing=timing)
+                if check <= WINDOW_CHECK_TOL or margin >= 4 * WINDOW_MARGIN:
+                    break
+                print(f'calc_and_parse_errors: window sigma moved by {check:.1e} with twice the margin '
+                      f'({margin} nodes); retrying with a margin of {2 * margin}', flush=True)
+                margin *= 2
+            if check > WINDOW_CHECK_TOL:
+                print(f'calc_and_parse_errors: WARNING window sigma within {check:.1e} only (margin {margin} nodes)',
+                      flush=True)
+            approx = (f'window (conditional variance): tile {WINDOW_TILE}, margin {margin} nodes, '
+                      f'self-check {check:.1e} relative at twice the margin')
             timing['decompose_qz'] = time() - tic
             off = 0
             for k, m in zip(keys, mats):
@@ -204,6 +229,8 @@ def calc_and_parse_errors(E, G_data, Gc, Ed, Ec, data, in_TSE, keep_cols, grids,
                                               'sigma_z0': np.reshape(E0[Gc.TOC['cols']['z0']], z0g.shape)})
     E['sigma_dz'] = pc.grid.data().from_dict({'x': dzg.ctrs[1], 'y': dzg.ctrs[0], 'time': dzg.ctrs[2],
                                               'sigma_dz': np.reshape(E0[Gc.TOC['cols']['dz']], dzg.shape)})
+    if approx is not None:
+        timing['E_approximate'] = approx
     if avg_ops:
         if Rinv is not None:
             full = np.zeros((Gc.col_N, Rinv.shape[1]))
@@ -213,4 +240,7 @@ def calc_and_parse_errors(E, G_data, Gc, Ed, Ec, data, in_TSE, keep_cols, grids,
             fields = {coord: ctr for coord, ctr in zip(op.dst_grid.coords, op.dst_grid.ctrs)}
             fields['sigma_' + key] = op.grid_error(Rs) if Rinv is not None else _grid_values(op, op_err[key])
             E['sigma_' + key] = pc.grid.data().from_dict(fields)
+    if approx is not None:   # every output grid says it is the windowed (conditional) variance
+        for v in E.values():
+            v.approximate = approx
     return E

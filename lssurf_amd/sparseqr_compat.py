@@ -88,6 +88,9 @@ def solve(A, b, tolerance=None, device=0, **opts):
 solve.last_stats = None
 
 
+NEAR_DEFICIENT = 1e-7
+
+
 def rz(A, b, tolerance=None, device=0):
     """Drop-in for PySPQR's ``sparseqr.rz(A, b)`` (LSsurf/smooth_fit.py:218): returns
     (Z, R, E, rank) with A[:, E] = Q·R, R upper triangular (scipy CSR), Z = Qᵀb, rank = n.
@@ -97,7 +100,13 @@ def rz(A, b, tolerance=None, device=0):
     (R is unique for full column rank once its diagonal is positive); Z = R⁻ᵀ(A E)ᵀb.  Everything
     the reference computes from rz — x = E·R⁻¹Z, R⁻¹ by inv_tr_upper, the error propagation — is
     the same.  ``tolerance`` (SPQR's rank tolerance) has no meaning here: A must have full column
-    rank (a rank-deficient A raises)."""
+    rank (a rank-deficient A raises).
+
+    Accuracy limit: R comes from a Cholesky factor of the normal matrix, which squares A's
+    condition number — where cond(A) approaches 1/sqrt(eps) ≈ 7e7 (e.g. the anisotropic notebook's
+    stiffest systems), R⁻¹ and Z lose digits that a QR of A would keep.  min |R_ii| / max |R_ii| is
+    checked: below NEAR_DEFICIENT (1e-7, i.e. cond(A) ≳ 1e7 in the diagonal's spread) a
+    RuntimeWarning says so."""
     from scipy.sparse.linalg import spsolve_triangular
     A = sp.csr_matrix(A)
     b = np.asarray(b, dtype=np.float64)
@@ -106,6 +115,12 @@ def rz(A, b, tolerance=None, device=0):
     with LSQSolver(device) as s:
         s.set_matrix_coo(A.shape[0], A.shape[1], coo.row, coo.col, coo.data)
         R, E = s.band_factor(perm)
+    d = np.abs(R.diagonal())
+    if d.size and d.min() < NEAR_DEFICIENT * d.max():
+        import warnings
+        warnings.warn(f'sparseqr_compat.rz: A is nearly rank deficient (min/max |R_ii| = {d.min() / d.max():.1e}); '
+                      f'R from the normal matrix loses about {-np.log10(d.min() / d.max()):.0f} digits against a QR '
+                      f'of A', RuntimeWarning, stacklevel=2)
     AE = A[:, E]
     Z = spsolve_triangular(R.T.tocsr(), AE.T @ b, lower=True)
     return Z, R, E, A.shape[1]

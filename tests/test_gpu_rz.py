@@ -13,7 +13,7 @@ from conftest import golden, golden_csr
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize('name', ['sf3d', 'aniso37'])
+@pytest.mark.parametrize('name', ['sf3d', 'aniso37', 'aniso41', 'aniso3d'])
 def test_rz_factor_and_solution(gpu_available, name):
     from lssurf_amd import sparseqr_compat as sq
     g = golden(f'sys_{name}.npz')
@@ -30,7 +30,11 @@ def test_rz_factor_and_solution(gpu_available, name):
     x = np.zeros(n)
     x[E] = y
     xs = g['x']
-    assert np.linalg.norm(x - xs) / np.linalg.norm(xs) <= 1e-9
+    # R is the Cholesky factor of the normal matrix: its forward error grows with cond(A)², which
+    # the spread of R's diagonal bounds from below (sparseqr_compat.rz docstring)
+    d = R.diagonal()
+    tol = max(1e-9, 100 * np.finfo(float).eps * (d.max() / d.min()) ** 2)
+    assert np.linalg.norm(x - xs) / np.linalg.norm(xs) <= tol
 
 
 def test_rz_feeds_the_reference_error_pipeline(gpu_available):

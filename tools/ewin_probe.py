@@ -26,12 +26,12 @@ def diag(name, tile, margin):
     from lssurf_amd.errors import _node_index
     S, fs, keep = system(name)
     Ef, _, info = fs.solver.cov_band(band_order(S['grids'], keep))
-    Ew, _ = window_cov(fs.solver, S['grids'], keep, tile=tile, margin=margin)
+    Ew, _, _ = window_cov(fs.solver, S['grids'], keep, tile=tile, margin=margin)
     iy, ix = _node_index(S['grids'], keep)
     z0n = S['grids']['z0'].N_nodes
     nt = S['grids']['dz'].shape[2]
     rel = np.abs(Ew - Ef) / Ef
-    Ewf, _ = window_cov(fs.solver, S['grids'], keep, tile=64, margin=0)   # one window = everything
+    Ewf, _, _ = window_cov(fs.solver, S['grids'], keep, tile=64, margin=0)   # one window = everything
     print('one-window vs full band max rel', float(np.max(np.abs(Ewf - Ef) / Ef)))
     if keep.size <= 60000:
         Ed = fs.solver.sigma_x()
@@ -63,7 +63,7 @@ for name in (sys.argv[1:] if __name__ == '__main__' else []):
         print(json.dumps({'name': name, 'full_band_s': tf, 'w': int(info[0])}), flush=True)
         for tile, margin in ((16, 4), (16, 8), (16, 12), (16, 16), (32, 16), (32, 24)):
             t0 = time.time()
-            Ew, _ = window_cov(fs.solver, S['grids'], keep, tile=tile, margin=margin)
+            Ew, _, _ = window_cov(fs.solver, S["grids"], keep, tile=tile, margin=margin)
             rel = np.abs(Ew - Ef) / Ef
             print(json.dumps({'name': name, 'tile': tile, 'margin': margin, 'time_s': time.time() - t0,
                               'max_rel': float(rel.max()), 'median_rel': float(np.median(rel)),
@@ -71,7 +71,7 @@ for name in (sys.argv[1:] if __name__ == '__main__' else []):
     else:
         tm = {}
         t0 = time.time()
-        Ew, _ = window_cov(fs.solver, S['grids'], keep, timing=tm)
+        Ew, _, _ = window_cov(fs.solver, S['grids'], keep, timing=tm)
         print(json.dumps({'name': name, 'n': int(keep.size), 'time_s': time.time() - t0, **tm,
                           'E_median': float(np.median(Ew)), 'E_min': float(Ew.min())}), flush=True)
     fs.close()
