@@ -343,6 +343,7 @@ def main():
             return {'solve_time_s': st['time_s'], 'solve_setup_s': st.get('setup_s', 0.0),
                     'solve_total_s': st['time_s'] + st.get('setup_s', 0.0),
                     'solve_iters': int(st['iters']), 'solve_istop': int(st['istop']),
+                    'solve_comm_bytes_per_iter': float(st.get('comm_bytes_per_iter', 0.0)),
                     'solve_iters_per_s': st['iters'] / st['time_s'] if st['time_s'] > 0 else None,
                     'solve_roofline': {'bytes_per_iter': st['bytes_per_iter'],
                                        'achieved_gbs': st['bytes_per_iter'] * st['iters'] / st['time_s'] / 1e9

@@ -82,6 +82,9 @@ typedef struct lsq_stats {
     double  setup_s;       /* CGNR: per-solve preconditioner set-up and initialisation (block   */
                            /*     factors, multigrid levels and λ estimates), host wall clock, */
                            /*     not part of time_s; LSQR: 0                                  */
+    double  comm_bytes_per_iter; /* distributed CGNR: bytes one rank sends per iteration (halos   */
+                           /*     and all-reduces; the busiest rank of a virtual / device group); */
+                           /*     0 on one GPU                                                  */
 } lsq_stats;
 
 void        lsq_default_opts(lsq_opts* o);

@@ -40,7 +40,8 @@ class LsqStats(ctypes.Structure):
     _fields_ = [('iters', ctypes.c_int64), ('istop', ctypes.c_int32), ('method', ctypes.c_int32),
                 ('r1norm', ctypes.c_double), ('r2norm', ctypes.c_double), ('anorm', ctypes.c_double),
                 ('acond', ctypes.c_double), ('arnorm', ctypes.c_double), ('xnorm', ctypes.c_double),
-                ('time_s', ctypes.c_double), ('bytes_per_iter', ctypes.c_double), ('setup_s', ctypes.c_double)]
+                ('time_s', ctypes.c_double), ('bytes_per_iter', ctypes.c_double), ('setup_s', ctypes.c_double),
+                ('comm_bytes_per_iter', ctypes.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
