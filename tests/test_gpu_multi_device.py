@@ -109,7 +109,9 @@ def test_smooth_fit_two_ranks_warm_start_and_device_outputs(gpu_available, monke
     (fewer CGNR iterations than the first); parse_model's constraint R / RMS and count / misfit maps
     come from the ranks' devices — the constraint operator is never converted to a host CSR
     (smooth_fit.py:324-345 on the host)."""
-    from lssurf_amd import lin_op as lo
+    import sys
+    import lssurf_amd.lin_op  # noqa: F401  (the package re-exports the class under the module's name)
+    lo = sys.modules['lssurf_amd.lin_op']
     calls = []
     orig = lo.lin_op.toCSR
 

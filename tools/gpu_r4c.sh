@@ -7,10 +7,15 @@ OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r4c}
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_SEL:-} > $OUT/gpu_tests.log 2>&1
 rc=$?; tail -3 $OUT/gpu_tests.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|error" $OUT/gpu_tests.log | head -20; exit 1; }
 timeout -k 10 300 python3 bench.py --config c4 --no-cpu --steps 200 --warmup 20 > $OUT/c4.json 2> $OUT/c4.err || exit 1
-python3 -c "import json; d=json.load(open('$OUT/c4.json')); print('c4', round(d['value']), 'frac', round(d['roofline']['frac'],3), 'MG', round(d['solve_time_s'],4), d['solve_iters'], 'setup', round(d['solve_setup_s'],4), 'form', round(d['device_formation_s'],3), 'bytes', d['config']['rank0_system']['device_bytes'])"
+python3 -c "import json; d=json.load(open('$OUT/c4.json')); print('c4', round(d['value']), 'frac', round(d['roofline']['frac'],3), {k: round(v*1e3,1) for k,v in d['roofline']['kernel_ms'].items()}, 'MG', round(d['solve_time_s'],4), d['solve_iters'], 'setup', round(d['solve_setup_s'],4), 'form', round(d['device_formation_s'],3), 'bytes', d['config']['rank0_system']['device_bytes'])"
+for v in "LSQ_CG_ATQ_RW=0" "LSQ_MG_PERSIST=4096 LSQ_MG_PWG=1" "LSQ_MG_PERSIST=16384 LSQ_MG_PWG=1"; do
+  tag=$(echo $v | tr ' =' '__')
+  env $v timeout -k 10 300 python3 bench.py --config c4 --no-cpu --no-pmc --steps 200 --warmup 20 > $OUT/c4_$tag.json 2> $OUT/c4_$tag.err || exit 1
+  python3 -c "import json; d=json.load(open('$OUT/c4_$tag.json')); print('c4 $v', round(d['value']), {k: round(v*1e3,1) for k,v in d['roofline']['kernel_ms'].items()}, 'MG', round(d['solve_time_s'],4), d['solve_iters'])"
+done
 DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu --no-pmc --steps 200 --warmup 20 > $OUT/prof.json 2> $OUT/prof.err
 echo "prof rc=$?"
 for n in 4 8; do
@@ -18,12 +23,4 @@ for n in 4 8; do
     LSQ_MG_PART=$part timeout -k 10 300 python3 tools/vgroup_bench.py c4 $n > $OUT/vg_c4_${n}_p$part.json 2> $OUT/vg_c4_${n}_p$part.err || { echo "vgroup $n $part failed"; exit 1; }
     cat $OUT/vg_c4_${n}_p$part.json
   done
-done
-for c in cf1e74e 33d1d38 5ce97ea 708e2d2 c74d764 fe9309c 86239f2 4a2b8fc; do
-  (cd tools/ab/bisect/$c && timeout -k 10 240 python3 bench.py --config c5a --no-cpu --no-pmc --steps 20 --warmup 5 > $OUT/c5a_$c.json 2> $OUT/c5a_$c.err) || { echo "c5a $c failed"; exit 1; }
-  python3 -c "import json; d=json.load(open('$OUT/c5a_$c.json')); print('c5a $c MG', d['solve_iters'], round(d['solve_time_s'],3), 'BJ', d.get('solve_block_jacobi',{}).get('solve_iters'))"
-done
-for v in "LSQ_CG_RW=0" "LSQ_CG_RW_KT=0" "LSQ_CG_DMF=0"; do
-  env $v timeout -k 10 240 python3 bench.py --config c5a --no-cpu --no-pmc --steps 20 --warmup 5 > $OUT/c5a_$v.json 2> $OUT/c5a_$v.err || exit 1
-  python3 -c "import json; d=json.load(open('$OUT/c5a_$v.json')); print('c5a $v MG', d['solve_iters'], round(d['solve_time_s'],3), 'BJ', d['solve_block_jacobi']['solve_iters'])"
 done
