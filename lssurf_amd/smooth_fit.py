@@ -19,6 +19,7 @@ NotImplementedError instead of silently changing the fit.
 """
 from time import ctime, time
 
+import warnings
 import numpy as np
 
 from . import containers as pc
@@ -487,6 +488,10 @@ def smooth_fit(**kwargs):
                 [args['device'] + k for k in range(int(args['n_gpus']))]
             if len(devices) > 1:   # y-slab ranks on several devices of this process (lssurf_amd.dist)
                 from .dist import MultiDeviceFitSystem
+                if len(set(devices)) > 1:
+                    warnings.warn('smooth_fit(n_gpus > 1) on distinct devices: the threaded device-group '
+                                  'path (one RCCL communicator per device) has been tested only as ranks '
+                                  'sharing one device; see INTEGRATION.md §5', RuntimeWarning, stacklevel=2)
                 system = MultiDeviceFitSystem(G_data, Gc, keep_cols, Gc.col_N, devices)
             else:
                 system = FitSystem(G_data, Gc, keep_cols, Gc.col_N, device=devices[0], grids=grids)

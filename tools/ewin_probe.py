@@ -61,11 +61,17 @@ for name in (sys.argv[1:] if __name__ == '__main__' else []):
         Ef, _, info = fs.solver.cov_band(band_order(S['grids'], keep))
         tf = time.time() - t0
         print(json.dumps({'name': name, 'full_band_s': tf, 'w': int(info[0])}), flush=True)
-        for tile, margin in ((16, 4), (16, 8), (16, 12), (16, 16), (32, 16), (32, 24)):
+        combos = ((16, 4), (16, 8), (16, 12), (16, 16), (32, 16), (32, 24))
+        if os.environ.get('EWIN_COMBOS'):
+            combos = [tuple(int(v) for v in c.split('/')) for c in os.environ['EWIN_COMBOS'].split(',')]
+        for tile, margin in combos:
             t0 = time.time()
             Ew, _, _ = window_cov(fs.solver, S["grids"], keep, tile=tile, margin=margin)
             rel = np.abs(Ew - Ef) / Ef
+            worst = int(np.argmax(rel))
             print(json.dumps({'name': name, 'tile': tile, 'margin': margin, 'time_s': time.time() - t0,
+                              'worst_col': worst, 'worst_Ew': float(Ew[worst]), 'worst_Ef': float(Ef[worst]),
+                              'frac_low': float(np.mean(Ew < Ef)),
                               'max_rel': float(rel.max()), 'median_rel': float(np.median(rel)),
                               'p99_rel': float(np.quantile(rel, 0.99))}), flush=True)
     else:
