@@ -137,6 +137,135 @@ __global__ __launch_bounds__(BLOCK) void k_block_normal_mf(int64_t nb, int kmax,
     }
 }
 
+// The same (AᵀA)_bb when every stencil part of the system has one row scale and constant
+// coefficients (smooth_fit's constraints): a node column's own entries of the stencil part depend
+// on the node only through its boundary class (as the CG's normal-stencil tables,
+// ns_from_parts in lsqr_cg.inc), so the part loop above — 64-bit index arithmetic and a
+// template-pair search per entry, 54 ms at C4 — becomes one table read per entry.  Table of grid
+// g: coef[coef0 + ((cy·ncls1 + cx)·ncls2 + ct)·BN_NDT + dt + BN_DT] (dt = t_j − t_i; the rows of
+// the class representative, summed in ns_from_parts' order: parts, t1, t2).
+constexpr int BN_DT = KB - 1, BN_NDT = 2 * BN_DT + 1;
+struct BnGrid {
+    int32_t col0, nodes, S[3], K[3], ncls[3], coef0;
+    FastDiv fd1, fd2;   // by shape[1] · shape[2] and by shape[2]
+};
+struct BnDesc {
+    int32_t n;
+    BnGrid g[MF_MAX_GRIDS];
+};
+__device__ __forceinline__ uint32_t bn_div(uint32_t n, const FastDiv& f) {
+    return (uint32_t)(((uint64_t)n * f.mul) >> (32 + f.shift));
+}
+__device__ __forceinline__ int bn_cls(int c, int n, int K, int ncls) {
+    return ncls == n ? c : (c < K ? c : (c >= n - K ? c - n + 2 * K + 1 : K));
+}
+__global__ __launch_bounds__(BLOCK) void k_block_normal_tab(int64_t nb, int kmax, const int64_t* __restrict__ ptr,
+                                                            const int32_t* __restrict__ cols,
+                                                            const int32_t* __restrict__ full,
+                                                            const int64_t* __restrict__ trp,
+                                                            const int32_t* __restrict__ tci,
+                                                            const double* __restrict__ tval,
+                                                            const double* __restrict__ rs, BnDesc D,
+                                                            const double* __restrict__ coef, double* __restrict__ N) {
+    const int npk = kmax * (kmax + 1) / 2;
+    const int64_t total = nb * npk;
+    for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < total; q += (int64_t)gridDim.x * BLOCK) {
+        const int64_t b = q / npk;
+        const int e = (int)(q - b * npk);
+        int j = 0;
+        while ((j + 1) * (j + 2) / 2 <= e) ++j;
+        const int i = e - j * (j + 1) / 2;
+        const int64_t b0 = ptr[b];
+        const int k = (int)(ptr[b + 1] - b0);
+        if (j >= k) {
+            N[q] = 0.0;
+            continue;
+        }
+        double s = col_dot(trp, tci, tval, rs, cols[b0 + i], cols[b0 + j]);
+        const int fi = full[b0 + i], fj = full[b0 + j];
+        for (int g = 0; g < D.n; ++g) {
+            const BnGrid& G = D.g[g];
+            if (fi < G.col0 || fi >= G.col0 + G.nodes) continue;
+            if (fj < G.col0 || fj >= G.col0 + G.nodes) break;
+            const uint32_t ri = (uint32_t)(fi - G.col0), rj = (uint32_t)(fj - G.col0);
+            const uint32_t ni = bn_div(ri, G.fd2), nj = bn_div(rj, G.fd2);   // (y, x) node
+            if (ni != nj) break;
+            const int ti = (int)(ri - ni * (uint32_t)G.S[2]), dt = (int)(rj - nj * (uint32_t)G.S[2]) - ti;
+            const uint32_t y = bn_div(ri, G.fd1);
+            const int x = (int)(ni - y * (uint32_t)G.S[1]);
+            const int cy = bn_cls((int)y, G.S[0], G.K[0], G.ncls[0]), cx = bn_cls(x, G.S[1], G.K[1], G.ncls[1]);
+            const int ct = bn_cls(ti, G.S[2], G.K[2], G.ncls[2]);
+            if (dt >= -BN_DT && dt <= BN_DT)
+                s += coef[G.coef0 + ((cy * G.ncls[1] + cx) * G.ncls[2] + ct) * BN_NDT + dt + BN_DT];
+            break;
+        }
+        N[q] = s;
+    }
+}
+
+// Host: the tables of k_block_normal_tab from the part descriptors; false when a part has per-row
+// scales or field-valued coefficients (then k_block_normal_mf)
+static int bn_rep(int k, int n, int K, int ncls) { return ncls == n ? k : (k <= K ? k : n - 2 * K - 1 + k); }
+bool block_normal_tables(const MfDesc& d, BnDesc& D, std::vector<double>& coef) {
+    D = BnDesc{};
+    coef.clear();
+    D.n = d.n_grids;
+    for (int g = 0; g < d.n_grids; ++g) {
+        const MfGrid& G = d.g[g];
+        BnGrid& B = D.g[g];
+        B.col0 = G.col0;
+        B.nodes = G.nparts ? G.nodes : 0;   // grids without parts: no stencil entries
+        for (int e = 0; e < 3; ++e) B.S[e] = G.ndim > e ? G.shape[e] : 1;
+        int K[3] = {0, 0, 0};
+        for (int qq = 0; qq < G.nparts; ++qq) {
+            const MfPart& P = d.p[G.part[qq]];
+            if (!P.wconst || P.var) return false;
+            for (int e = 0; e < 3; ++e) {
+                int omin = 1 << 20, omax = -(1 << 20);
+                for (int t = 0; t < P.ntpl; ++t) {
+                    omin = std::min(omin, P.off[t][e]);
+                    omax = std::max(omax, P.off[t][e]);
+                }
+                K[e] = std::max({K[e], P.lo[e] + omax, B.S[e] - P.hi[e] - omin, 0});
+            }
+        }
+        for (int e = 0; e < 3; ++e) {
+            B.K[e] = K[e];
+            B.ncls[e] = B.S[e] <= 2 * K[e] + 1 ? B.S[e] : 2 * K[e] + 1;
+        }
+        B.fd1 = make_fastdiv((uint32_t)B.S[1] * (uint32_t)B.S[2]);
+        B.fd2 = make_fastdiv((uint32_t)B.S[2]);
+        B.coef0 = (int32_t)coef.size();
+        if (!G.nparts) continue;
+        coef.resize(coef.size() + (size_t)B.ncls[0] * B.ncls[1] * B.ncls[2] * BN_NDT, 0.0);
+        for (int cy = 0; cy < B.ncls[0]; ++cy)
+            for (int cx = 0; cx < B.ncls[1]; ++cx)
+                for (int ct = 0; ct < B.ncls[2]; ++ct) {
+                    const int pos[3] = {bn_rep(cy, B.S[0], K[0], B.ncls[0]), bn_rep(cx, B.S[1], K[1], B.ncls[1]),
+                                        bn_rep(ct, B.S[2], K[2], B.ncls[2])};
+                    double* row = coef.data() + B.coef0 + ((size_t)(cy * B.ncls[1] + cx) * B.ncls[2] + ct) * BN_NDT;
+                    for (int qq = 0; qq < G.nparts; ++qq) {
+                        const MfPart& P = d.p[G.part[qq]];
+                        for (int t1 = 0; t1 < P.ntpl; ++t1) {
+                            bool in = true;   // the row centred at pos − o_t1 exists
+                            for (int e = 0; e < 3; ++e) {
+                                const int ce = pos[e] - P.off[t1][e];
+                                in = in && ce >= P.lo[e] && ce < P.hi[e];
+                            }
+                            if (!in) continue;
+                            for (int t2 = 0; t2 < P.ntpl; ++t2) {
+                                if (P.off[t2][0] != P.off[t1][0] || P.off[t2][1] != P.off[t1][1]) continue;
+                                const int dt = P.off[t2][2] - P.off[t1][2];
+                                if (dt < -BN_DT || dt > BN_DT) continue;   // beyond any block
+                                row[dt + BN_DT] += (P.w * P.val[t1]) * (P.w * P.val[t2]);
+                            }
+                        }
+                    }
+                }
+    }
+    return true;
+}
+
 // In place: N_b -> R_b (Cholesky, upper) -> R_b⁻¹, one thread per block
 __global__ __launch_bounds__(BLOCK) void k_block_factor(int64_t nb, const int64_t* __restrict__ ptr, int kmax,
                                                         double* __restrict__ Ri, unsigned long long* ndead) {
@@ -277,7 +406,16 @@ void block_normal(System& S) {
     ensure_blocks(S);
     const int npk = S.blk_kmax * (S.blk_kmax + 1) / 2;
     if (S.blk_Ri.n != (int64_t)npk * S.nblk) S.blk_Ri.alloc((int64_t)npk * S.nblk);
-    if (!S.g_full)   // lazily formed structured system: GdT + the stencil parts
+    BnDesc bd;
+    std::vector<double> tab;
+    const bool tab_env = !(getenv("LSQ_BLK_TAB") && getenv("LSQ_BLK_TAB")[0] == '0');   // A/B + parity test (per call)
+    if (!S.g_full && tab_env && block_normal_tables(S.mfh, bd, tab)) {   // lazily formed, class tables
+        S.blk_tab.alloc(std::max<int64_t>((int64_t)tab.size(), 1));
+        S.blk_tab.upload(tab.data(), (int64_t)tab.size(), S.stream);
+        hipLaunchKernelGGL(k_block_normal_tab, dim3(grid_for(S.nblk * npk)), dim3(BLOCK), 0, S.stream, S.nblk,
+                           S.blk_kmax, S.blk_ptr.p, S.blk_cols.p, S.blk_full.p, S.GdT.rp.p, S.GdT.ci.p, S.GdT.val.p,
+                           S.rs.p, bd, S.blk_tab.p, S.blk_Ri.p);
+    } else if (!S.g_full)   // lazily formed structured system: GdT + the stencil parts
         hipLaunchKernelGGL(k_block_normal_mf, dim3(grid_for(S.nblk * npk)), dim3(BLOCK), 0, S.stream, S.nblk,
                            S.blk_kmax, S.blk_ptr.p, S.blk_cols.p, S.blk_full.p, S.GdT.rp.p, S.GdT.ci.p, S.GdT.val.p,
                            S.mfd.p, S.rs.p, S.blk_Ri.p);

@@ -1,5 +1,5 @@
 """The row-streaming node gather of the matrix-free data rows (k_cg_dmf_atq_rw, round 4) against
-the per-node kernel it replaces (k_cg_dmf_atq, LSQ_CG_ATQ_RW=0, read at every launch): q += Adᵀt
+the per-node kernel (k_cg_dmf_atq, the default; LSQ_CG_ATQ_RW=0 / 1 read at every launch): q += Adᵀt
 sums every node's points in the same order with the same products, so the two are equal BIT FOR
 BIT — through lsq_data_colsum (parse_model's count / misfit maps) on random per-point values and
 through the normal operator q = AᵀA p, on grids whose node rows are not a multiple of the wave's
