@@ -2,7 +2,7 @@
 
 Domain W_x = W_y = (n-1)*100 m centred on 0, spacing z0 = dz = 100 m (Z0_REFINED: z0 50 m), dt = 0.25,
 W_t = (nt-1)*0.25, reference_epoch = nt//2; points uniform in (x, y, t) from
-default_rng(20251121 + config_id); z = 10 sin(2πx/Lx) cos(2πy/Ly) + 0.5 t exp(-r²/(W/4)²)
+default_rng(20251121 + SEED_ID[config]); z = 10 sin(2πx/Lx) cos(2πy/Ly) + 0.5 t exp(-r²/(W/4)²)
 + N(0, 0.1), Lx = W/2, Ly = W/3, sigma = 0.1; E_RMS = notebook cell-17 set.
 """
 import numpy as np
@@ -38,6 +38,12 @@ CONFIGS = {
     't64z': (64, 12, 8_192),
     'c3z': (512, 12, 1_000_000),
 }
+# seed offset of each config's points (default_rng(20251121 + id)): the configs' positions in
+# CONFIGS when round 4 started, frozen — round 3 derived the offset from the dict position, so
+# inserting 't128' moved every later config onto new points (C5a: 61 → 72 multigrid iterations
+# between two builds that solve the same system alike).  New configs take new ids.
+SEED_ID = {'c1': 0, 'c3': 1, 'c4': 2, 'c5': 3, 't64': 4, 't256': 5, 't128': 6, 'tdense': 7, 't15': 8,
+           'c4y4': 9, 'c4y8': 10, 'c5a': 11, 'ta64': 12, 'ta100': 13, 't64z': 14, 'c3z': 15}
 ANISO = ('c5a', 'ta64', 'ta100')
 Z0_REFINED = ('t64z', 'c3z')
 
@@ -53,7 +59,7 @@ def config_kwargs(name, stiff=False):
 
 def points(name, config_id=None):
     kw, npts = config_kwargs(name)
-    cid = list(CONFIGS).index(name) if config_id is None else config_id
+    cid = SEED_ID[name] if config_id is None else config_id
     rng = np.random.default_rng(20251121 + cid)
     W, ctr = kw['W'], kw['ctr']
     x = ctr['x'] + (rng.random(npts) - 0.5) * W['x']
@@ -102,10 +108,10 @@ def system2d(name):
     return G, Gc, g, 1. / E_all, rhs
 
 
-def aniso_system(name, stiff=False):
+def aniso_system(name, stiff=False, config_id=None):
     """lssurf_amd.aniso.system3d on the synthetic points of an anisotropic config (ANISO)."""
     from . import aniso
-    D, kw = points(name)
+    D, kw = points(name, config_id)
     if stiff:
         kw['E_RMS'] = dict(E_RMS_STIFF)
     return aniso.system3d(D, **kw), kw

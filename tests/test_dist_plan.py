@@ -222,3 +222,13 @@ def test_window_problem_slices_field_values():
         assert prob['halo'] >= 1
     allrows = np.sort(np.concatenate(seen))
     assert np.array_equal(allrows, np.arange(S['w'].size))
+
+
+def test_synthetic_seed_ids_frozen():
+    """Every synthetic config has its own frozen seed offset (SEED_ID), independent of the order of
+    CONFIGS: a config added anywhere must not move the points of the others (round 3's position-
+    derived offsets did: C5a's cloud changed under the benchmark)."""
+    from lssurf_amd import synthetic
+    assert set(synthetic.SEED_ID) == set(synthetic.CONFIGS)
+    assert len(set(synthetic.SEED_ID.values())) == len(synthetic.SEED_ID)
+    assert synthetic.SEED_ID['c4'] == 2 and synthetic.SEED_ID['c5a'] == 11

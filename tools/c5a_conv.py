@@ -4,7 +4,7 @@ after k iterations for a range of k, and the iteration count at several atol.  A
 61 → 72 iteration change between two builds is a plateau of the ratio near atol = 1e-10 (a rounding-
 level perturbation moves the stop) or a weaker preconditioner.
 
-    python tools/c5a_conv.py [config]"""
+    python tools/c5a_conv.py [config [seed id]]"""
 import json
 import os
 import sys
@@ -14,10 +14,10 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main(cfg):
+def main(cfg, seed=None):
     from lssurf_amd import synthetic
     from lssurf_amd.smooth_fit import FitSystem
-    S, _ = synthetic.aniso_system(cfg)
+    S, _ = synthetic.aniso_system(cfg) if seed is None else synthetic.aniso_system(cfg, config_id=seed)
     fs = FitSystem(S['G_data'], S['Gc'], S['keep'], S['Gc'].col_N, grids=S['grids'])
     try:
         fs.solver.set_row_weight(S['w'])
@@ -38,4 +38,4 @@ def main(cfg):
 
 
 if __name__ == '__main__':
-    main(sys.argv[1] if len(sys.argv) > 1 else 'c5a')
+    main(sys.argv[1] if len(sys.argv) > 1 else 'c5a', int(sys.argv[2]) if len(sys.argv) > 2 else None)
