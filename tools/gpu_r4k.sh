@@ -5,7 +5,7 @@ OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r4k}
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest tests/test_gpu_dfuse.py tests/test_gpu_cgnr.py tests/test_gpu_mg.py tests/test_gpu_atq_rw.py tests/test_gpu_smooth_fit.py -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+timeout -k 10 500 python -u -m pytest tests/test_gpu_dfuse.py tests/test_gpu_cgnr.py tests/test_gpu_mg.py tests/test_gpu_atq_rw.py tests/test_gpu_dist.py tests/test_gpu_dist_rccl.py tests/test_gpu_smooth_fit.py -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
 rc=$?; tail -2 $OUT/gpu_tests.log; grep -E "^FAILED|^ERROR|^E  " $OUT/gpu_tests.log | head -20
 [ $rc -le 1 ] || exit 1
 for v in "LSQ_CG_DFUSE=1" "LSQ_CG_DFUSE=0"; do
