@@ -248,32 +248,3 @@ def test_mg_persistent_coarse_levels(gpu_available, tmp_path):
         fs.close()
     assert abs(int(got[0]) - it) <= 1, (got[0], it)
     assert np.linalg.norm(got[1:] - x) <= 1e-8 * np.linalg.norm(x)
-
-
-@pytest.mark.parametrize('which', ['t64', 't256', 'tdense'])
-def test_mg_row_transfers_match_column_kernels(gpu_available, which):
-    """The row-streaming restriction / prolongation (k_mg_restrict_rows, k_mg_prolong_rows, round 4)
-    against the per-column kernels (LSQ_MG_ROWS=0, read per V-cycle): the prolongation sums in the
-    same order, the restriction separably (½h(2Y−1) + h(2Y) + ½h(2Y+1) of row sums) — the V-cycle
-    agrees to rounding."""
-    import os
-    S, fs, w, rhs = _synthetic_system(which)
-    rng = np.random.default_rng(11)
-    saved = os.environ.get('LSQ_MG_ROWS')
-    try:
-        _prepare(fs, w, np.ones(fs.n_data, bool))
-        nf = fs.n_full
-        u = np.zeros(nf)
-        u[fs.keep_cols] = rng.standard_normal(fs.keep_cols.size)
-        os.environ['LSQ_MG_ROWS'] = '0'
-        Va = fs.solver.mg_apply(0, 1, u)
-        os.environ['LSQ_MG_ROWS'] = '1'
-        Vb = fs.solver.mg_apply(0, 1, u)
-    finally:
-        if saved is None:
-            os.environ.pop('LSQ_MG_ROWS', None)
-        else:
-            os.environ['LSQ_MG_ROWS'] = saved
-        fs.close()
-    rel = np.linalg.norm(Vb - Va) / np.linalg.norm(Va)
-    assert 0.0 < rel <= 1e-12, rel   # the row kernels ran (a different summation) and agree
