@@ -51,47 +51,3 @@ def test_atq_rw_bitwise_equal(gpu_available, which):
         np.testing.assert_array_equal(qa, qb)
     finally:
         fs.close()
-
-
-def _env(val, fn):
-    saved = os.environ.get('LSQ_CG_ATQ_RW')
-    try:
-        if val is None:
-            os.environ.pop('LSQ_CG_ATQ_RW', None)
-        else:
-            os.environ['LSQ_CG_ATQ_RW'] = val
-        return fn()
-    finally:
-        if saved is None:
-            os.environ.pop('LSQ_CG_ATQ_RW', None)
-        else:
-            os.environ['LSQ_CG_ATQ_RW'] = saved
-
-
-@pytest.mark.parametrize('which', ['sf3d', 't64', 't256', 'tdense'])
-def test_atq_four_lanes_per_node(gpu_available, which):
-    """The default node gather (k_cg_dmf_atq4: one lane per cell of a node, the four cell sums
-    combined pairwise) against the one-lane kernel (LSQ_CG_ATQ_RW=0): the same products summed in
-    another order — equal to rounding (≤ 1e-13 of the column's magnitude) through lsq_data_colsum
-    and the normal operator."""
-    if which.startswith('t'):
-        _, fs, w, rhs = _synthetic_system(which)
-    else:
-        _, fs, w, rhs = _golden_system(which)
-    try:
-        fs.solver.set_row_weight(w)
-        fs.solver.set_row_mask(np.ones(w.size, bool))
-        rng = np.random.default_rng(4)
-        f = rng.standard_normal(fs.n_data)
-        a = _env('0', lambda: fs.solver.data_colsum(f))
-        b = _env(None, lambda: fs.solver.data_colsum(f))
-        scale = np.abs(f).max() * 4.0
-        assert np.abs(a - b).max() <= 1e-13 * scale
-        assert not np.array_equal(a, b) or which == 'sf3d'   # the four-lane kernel ran (another order)
-        p = np.zeros(fs.n_full)
-        p[fs.keep_cols] = rng.standard_normal(fs.keep_cols.size)
-        qa = _env('0', lambda: fs.solver.normal_apply(p))
-        qb = _env(None, lambda: fs.solver.normal_apply(p))
-        assert np.linalg.norm(qb - qa) <= 1e-13 * np.linalg.norm(qa)
-    finally:
-        fs.close()
