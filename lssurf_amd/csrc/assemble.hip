@@ -500,6 +500,7 @@ void form_from_stencils(System& S, int64_t m, int64_t n_full, int32_t n_grids, c
 
 void ensure_full_csr(System& S) {
     if (S.g_full) return;
+    graph_cache_drop(&S);   // G is reallocated (a captured batch may hold the data-row CSR's pointers)
     gen_rows_csr(S, S.gen_py.p, S.gen_px.p, S.gen_pt.n ? S.gen_pt.p : nullptr, S.G.m);
     S.g_full = true;
     S.gen_py = DBuf<double>();

@@ -802,6 +802,7 @@ void band_factor(System& S, const int32_t* h_perm, BandFactor& F, int64_t nw) {
     F.n = n;
     F.T = T;
     F.w = w;
+    graph_cache_drop(&S);   // a captured band-preconditioned LSQR batch holds the old factor's pointers
     F.R.alloc(band_tiles * TT);
     F.D.alloc(T * TT);
     F.sc.alloc(npad);

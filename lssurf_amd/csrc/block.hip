@@ -405,7 +405,10 @@ void ensure_blocks(System& S) {
 void block_normal(System& S) {
     ensure_blocks(S);
     const int npk = S.blk_kmax * (S.blk_kmax + 1) / 2;
-    if (S.blk_Ri.n != (int64_t)npk * S.nblk) S.blk_Ri.alloc((int64_t)npk * S.nblk);
+    if (S.blk_Ri.n != (int64_t)npk * S.nblk) {
+        graph_cache_drop(&S);   // captured block-preconditioned batches hold the old pointers
+        S.blk_Ri.alloc((int64_t)npk * S.nblk);
+    }
     BnDesc bd;
     std::vector<double> tab;
     const bool tab_env = !(getenv("LSQ_BLK_TAB") && getenv("LSQ_BLK_TAB")[0] == '0');   // A/B + parity test (per call)
@@ -433,7 +436,10 @@ void block_factor_in_place(System& S) {
                        S.blk_kmax, S.blk_Ri.p, nd.p);
     KERNEL_CHECK();
     const int npk = S.blk_kmax * (S.blk_kmax + 1) / 2, npks = lf_stride(npk);   // CGNR's copy
-    if (S.blk_Lf.n != (int64_t)npks * S.nblk) S.blk_Lf.alloc((int64_t)npks * S.nblk);
+    if (S.blk_Lf.n != (int64_t)npks * S.nblk) {
+        graph_cache_drop(&S);
+        S.blk_Lf.alloc((int64_t)npks * S.nblk);
+    }
     hipLaunchKernelGGL(k_block_rinv32, dim3(grid_for(S.nblk * npks)), dim3(BLOCK), 0, S.stream, S.nblk, npk, npks,
                        S.blk_Ri.p, S.blk_Lf.p);
     KERNEL_CHECK();

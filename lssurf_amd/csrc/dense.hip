@@ -303,6 +303,7 @@ void dense_factor(System& S) {
     const int64_t npad = (n + TB - 1) / TB * TB, ld = npad;
     const int nb = (int)(npad / TB);
     if (S.dR.n != npad * npad) {
+        graph_cache_drop(&S);   // captured dense-preconditioned batches hold the old pointers
         S.dR.alloc(npad * npad);
         S.dRi.alloc(npad * npad);
     }
