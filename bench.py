@@ -125,11 +125,20 @@ class _Dist:
         return d
 
 
-def cpu_baseline(fs, b_weighted, sample_iters, threads):
-    """oracle/lsqr_cpu.c on the same formed A (downloaded from the device) and the same
-    weighted rhs; a bounded sample of iterations, timed on this host's cores."""
+def cpu_baseline(fs, b_weighted, sample_iters, threads, method=0):
+    """The same algorithm on this host's cores, on the same formed A (downloaded from the device)
+    and the same weighted rhs, a bounded sample of iterations: CGNR + block-Jacobi with the GPU
+    solve's node blocks (oracle/cgnr_cpu.c) when the GPU line is CGNR, else LSQR
+    (oracle/lsqr_cpu.c)."""
     from oracle import cpu
     A = fs.solver.get_csr()
+    if method == 1 and getattr(fs, 'blocks', None) is not None:
+        x, st = cpu.cgnr_bj(A, b_weighted, *fs.blocks, fixed_iters=sample_iters, threads=threads)
+        return {'value': st['iters'] / st['time_s'], 'unit': 'CGNR iters/s', 'cores': int(st['threads']),
+                'kind': 'port', 'setup_s': st['setup_s'],
+                'sample': f'{int(st["iters"])} CGNR + block-Jacobi iterations of the same system and node blocks '
+                          f'(oracle/cgnr_cpu.c, OpenMP; the GPU line\'s algorithm), {st["time_s"]:.1f} s '
+                          f'after {st["setup_s"]:.1f} s of transpose and block factors'}
     x, st = cpu.lsqr(A, b_weighted, fixed_iters=sample_iters, threads=threads)
     return {'value': st['iters'] / st['time_s'], 'unit': 'LSQR iters/s', 'cores': int(st['threads']),
             'kind': 'port', 'sample': f'{int(st["iters"])} LSQR iterations of the same system (oracle/lsqr_cpu.c, '
@@ -220,7 +229,7 @@ def main():
     ap.add_argument('--config', default='c4')
     ap.add_argument('--no-solve', action='store_true', help='skip the full solve to tolerance')
     ap.add_argument('--cpu-iters', type=int, default=80,
-                    help='LSQR iterations of the CPU baseline sample (~11 s on 16 host threads at C4)')
+                    help='iterations of the CPU baseline sample (the GPU line\'s algorithm: CGNR + block-Jacobi, or LSQR)')
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--cpu-solve', action='store_true',
                     help='also run the CPU oracle LSQR to the solve tolerance (BASELINE.md §4 parity at size; slow)')
@@ -375,7 +384,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not args.dist:
         threads = min(os.cpu_count() or 1, 16)
-        cpu = cpu_baseline(fs, w * rhs, args.cpu_iters, threads)
+        cpu = cpu_baseline(fs, w * rhs, args.cpu_iters, threads, meth)
         if args.cpu_solve and solve:   # the CPU oracle to the same stopping rule, on the same A, b
             from oracle import cpu as ocpu
             xc, stc = ocpu.lsqr(fs.solver.get_csr(), w * rhs, atol=1e-10, btol=1e-10, conlim=1e8,

@@ -83,6 +83,7 @@ class FitSystem:
             if blocks is not None:
                 self.solver.set_column_blocks_csr(*blocks)
                 self.has_blocks = True
+                self.blocks = blocks   # (block_ptr, cols): bench.py's algorithm-matched CPU baseline
         self._mg = None            # multigrid (precond 4) availability, probed on first use
         self.mg_build_s = 0.0
         self.stats = None

@@ -19,6 +19,7 @@ for k in inv_tr_upper propagate_qz_errors spsolve_tr_upper; do
     cython -3 -o "$out/$k.c" "$src/$k.pyx"
     gcc -shared -fPIC -O2 -w -I"$inc_py" -I"$inc_np" -DNPY_NO_DEPRECATED_API=NPY_1_7_API_VERSION \
         -o "$out/$k$suf" "$out/$k.c"
+    rm -f "$out/$k.c"   # the generated C is an intermediate: only the built module is kept
   fi
 done
 echo "build_ref: built $(ls "$out"/*"$suf" | wc -l) reference kernels into $out"

@@ -1,6 +1,6 @@
 """ctypes wrappers for the oracle's C restatements (TEST INFRASTRUCTURE ONLY).
 
-build() compiles oracle/lsqr_cpu.c + oracle/tri_upper.c into oracle/_cpu.so with gcc -O2
+build() compiles oracle/lsqr_cpu.c + oracle/cgnr_cpu.c + oracle/tri_upper.c into oracle/_cpu.so with gcc -O2
 -fopenmp (no -march: plain SSE2 doubles, no FMA — matching the reference's Cython build).
 """
 import ctypes
@@ -12,7 +12,7 @@ import scipy.sparse as sp
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, '_cpu.so')
-SRC = [os.path.join(HERE, 'lsqr_cpu.c'), os.path.join(HERE, 'tri_upper.c')]
+SRC = [os.path.join(HERE, 'lsqr_cpu.c'), os.path.join(HERE, 'cgnr_cpu.c'), os.path.join(HERE, 'tri_upper.c')]
 _lib = None
 
 
@@ -33,6 +33,8 @@ def lib():
         i64, i32, f64, f32 = ctypes.c_int64, ctypes.c_int32, ctypes.c_double, ctypes.c_float
         L.lsqr_cpu.argtypes = [i64, i64, P, P, P, P, P, f64, f64, f64, i64, ctypes.c_int, i64, ctypes.c_int, P]
         L.lsqr_cpu.restype = ctypes.c_int
+        L.cgnr_bj_cpu.argtypes = [i64, i64, P, P, P, P, i64, P, P, P, f64, i64, i64, ctypes.c_int, P]
+        L.cgnr_bj_cpu.restype = ctypes.c_int
         L.oracle_inv_tr_upper.argtypes = [i64, P, P, P, i64, f32, P, P, P, P]
         L.oracle_inv_tr_upper.restype = ctypes.c_int
         L.oracle_propagate_qz_errors.argtypes = [i64, P, P, P, P]
@@ -62,6 +64,23 @@ def lsqr(A, b, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, fixed_ite
     lib().lsqr_cpu(m, n, _p(rp), _p(ci), _p(v), _p(b), _p(x), atol, btol, conlim, maxit, precond, fixed_iters,
                    threads, _p(st))
     keys = ['iters', 'istop', 'r1norm', 'r2norm', 'anorm', 'acond', 'arnorm', 'xnorm', 'time_s', 'threads']
+    return x, dict(zip(keys, st.tolist()))
+
+
+def cgnr_bj(A, b, block_ptr, block_cols, atol=1e-10, maxit=0, fixed_iters=0, threads=0):
+    """CPU CGNR + block-Jacobi (oracle/cgnr_cpu.c) on the final weighted A with the GPU solve's
+    column blocks (compact ids); returns (x, stats dict)."""
+    (m, n), rp, ci, v = _csr(A)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    bp = np.ascontiguousarray(block_ptr, dtype=np.int64)
+    bc = np.ascontiguousarray(block_cols, dtype=np.int32)
+    x = np.zeros(n)
+    st = np.zeros(7)
+    rc = lib().cgnr_bj_cpu(m, n, _p(rp), _p(ci), _p(v), _p(b), bp.size - 1, _p(bp), _p(bc), _p(x), atol, maxit,
+                           fixed_iters, threads, _p(st))
+    if rc != 0:
+        raise ValueError('cgnr_bj: a block has more than 16 columns')
+    keys = ['iters', 'time_s', 'setup_s', 'threads', 'snorm', 'rnorm', 'anorm_f']
     return x, dict(zip(keys, st.tolist()))
 
 
