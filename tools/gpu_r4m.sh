@@ -5,6 +5,8 @@ OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r4m}
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
+timeout -k 10 600 python3 bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err || { echo "default bench failed"; tail -5 $OUT/bench_default.err; exit 1; }
+python3 -c "import json; d=json.load(open('$OUT/bench_default.json')); print('default', round(d['value']), d['roofline'], d['cpu_baseline'])"
 for c in c4y4 c4y8; do
   timeout -k 10 300 python3 bench.py --config $c --dist --no-cpu --no-pmc --steps 200 --warmup 20 > $OUT/${c}_dist1.json 2> $OUT/${c}_dist1.err || { echo "$c failed"; tail -5 $OUT/${c}_dist1.err; exit 1; }
   python3 -c "import json; d=json.load(open('$OUT/${c}_dist1.json')); print('$c', round(d['value']), 'MG', round(d['solve_time_s'],4), d['solve_iters'], 'BJ', d.get('solve_block_jacobi',{}).get('solve_iters'), round(d.get('solve_block_jacobi',{}).get('solve_time_s',0),4))"
