@@ -92,6 +92,40 @@ def build_reference_epoch_matrix(G_data, Gc, grids, reference_epoch, dz_mask=Non
     return sp.coo_matrix((np.ones_like(keep), (keep, np.arange(keep.size))), shape=(Gc.col_N, keep.size)).tocsc()
 
 
+def _node_column_blocks_uniform(z0, dz, keep_cols, max_block):
+    """node_column_blocks' usual case — the same kept columns at every node, one block per node
+    (≤ max_block columns) — from views of the compact-position map (int32, no (nodes × k) index
+    arrays): the same (block_ptr, cols); None when the case does not apply."""
+    ny, nx, nt = (int(s) for s in dz.shape)
+    nn = ny * nx
+    same = z0 is not None and tuple(z0.shape) == (ny, nx) and all(
+        np.array_equal(a, b) for a, b in zip(z0.ctrs, dz.ctrs[:2]))
+    n_full = max(int(dz.col_0) + nn * nt, int(z0.col_0) + nn if same else 0,
+                 int(keep_cols.max()) + 1 if keep_cols.size else 0)
+    if n_full >= 2 ** 31 or keep_cols.size == 0:
+        return None
+    where = np.full(n_full, -1, dtype=np.int32)
+    where[keep_cols] = np.arange(keep_cols.size, dtype=np.int32)
+    wdz = where[int(dz.col_0):int(dz.col_0) + nn * nt].reshape(nn, nt)
+    tkeep = wdz[0] >= 0
+    if not np.array_equal(wdz >= 0, np.broadcast_to(tkeep, wdz.shape)):
+        return None
+    zk = False
+    if same:
+        wz = where[int(z0.col_0):int(z0.col_0) + nn]
+        zk = bool(wz[0] >= 0)
+        if not np.all((wz >= 0) == zk):
+            return None
+    k = int(tkeep.sum()) + (1 if zk else 0)
+    if k == 0 or k > max_block:
+        return None
+    cols = np.empty((nn, k), dtype=np.int32)
+    if zk:
+        cols[:, 0] = wz
+    cols[:, int(zk):] = wdz[:, tkeep]
+    return np.arange(0, (nn + 1) * k, k, dtype=np.int64), cols.ravel()
+
+
 def node_column_blocks(grids, keep_cols, max_block=16):
     """Column blocks of the block-Jacobi preconditioner (lsq precond 3):
     one block per (y, x) node = its z0 column (when the z0 and dz grids share the node lattice)
@@ -103,6 +137,9 @@ def node_column_blocks(grids, keep_cols, max_block=16):
         return None
     keep_cols = np.asarray(keep_cols)
     ny, nx, nt = (int(s) for s in dz.shape)
+    fast = _node_column_blocks_uniform(z0, dz, keep_cols, max_block)
+    if fast is not None:
+        return fast
     nodes = np.arange(ny * nx)
     dz_cols = dz.col_0 + nodes[:, None] * nt + np.arange(nt)[None, :]          # (nodes, nt) full ids
     same = z0 is not None and tuple(z0.shape) == (ny, nx) and all(

@@ -232,3 +232,25 @@ def test_synthetic_seed_ids_frozen():
     assert set(synthetic.SEED_ID) == set(synthetic.CONFIGS)
     assert len(set(synthetic.SEED_ID.values())) == len(synthetic.SEED_ID)
     assert synthetic.SEED_ID['c4'] == 2 and synthetic.SEED_ID['c5a'] == 11
+
+
+def test_node_column_blocks_uniform_fast_path():
+    """node_column_blocks' fast path (the same kept columns at every node: views of the compact-
+    position map) returns exactly what the general path does — shared lattice, 15 epochs, z0 on a
+    2× refinement (dz-only blocks)."""
+    from lssurf_amd import constraint_functions as cf
+    import lssurf_amd as LS
+    for name in ('t64', 't15', 't64z'):
+        D, kw = synthetic.points(name)
+        S = LS.smooth_fit(data=D, return_fit_objects=True, VERBOSE=False, **kw)
+        keep = np.asarray(cf.reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch']))
+        fast = cf._node_column_blocks_uniform(S['grids']['z0'], S['grids']['dz'], keep, 16)
+        assert fast is not None, name
+        saved = cf._node_column_blocks_uniform
+        try:
+            cf._node_column_blocks_uniform = lambda *a: None
+            ref = cf.node_column_blocks(S['grids'], keep)
+        finally:
+            cf._node_column_blocks_uniform = saved
+        assert np.array_equal(fast[0], ref[0]) and np.array_equal(fast[1], ref[1]), name
+        assert fast[1].dtype == np.int32 and fast[0].dtype == np.int64
