@@ -220,14 +220,7 @@ int lsq_set_column_blocks(lsq_handle* h, int64_t n_blocks, const int64_t* block_
 int lsq_set_row_mask(lsq_handle* h, const uint8_t* keep) {
     return guarded(h, [&](lsq::System& S) {
         if (!S.G.rp.p) return fail(S, "lsq_set_row_mask: no matrix");
-        if (keep) {
-            std::vector<uint8_t> k(keep, keep + S.G.m);
-            for (auto& x : k) x = x ? 1 : 0;
-            S.rowkeep.upload(k.data(), S.G.m, S.stream);
-        } else {
-            HIP_CHECK(hipMemsetAsync(S.rowkeep.p, 1, S.G.m, S.stream));
-        }
-        HIP_CHECK(hipStreamSynchronize(S.stream));
+        lsq::upload_row_mask(S, keep);
         S.rs_dirty = true;
         return 0;
     });

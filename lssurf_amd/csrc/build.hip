@@ -361,6 +361,10 @@ __global__ __launch_bounds__(BLOCK) void k_cs_finish(int64_t n, double* __restri
     }
 }
 
+__global__ __launch_bounds__(BLOCK) void k_mask01(int64_t n, uint8_t* __restrict__ k) {
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) k[i] = k[i] ? 1 : 0;
+}
+
 __global__ __launch_bounds__(BLOCK) void k_fill(int64_t n, double v, double* __restrict__ a) {
     for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) a[i] = v;
 }
@@ -834,6 +838,18 @@ void scaling_fill_values(System& S, int precond, bool set_csf) {
     S.rs_dirty = false;
     S.cs_mode = precond;
     S.iter_ready = false;
+}
+
+// row mask from the host (any non-zero byte keeps the row): uploaded as given, 0/1 on the device
+void upload_row_mask(System& S, const uint8_t* keep) {
+    if (keep) {
+        S.rowkeep.upload(keep, S.G.m, S.stream);
+        hipLaunchKernelGGL(k_mask01, dim3(grid_for(S.G.m)), dim3(BLOCK), 0, S.stream, S.G.m, S.rowkeep.p);
+        KERNEL_CHECK();
+    } else {
+        HIP_CHECK(hipMemsetAsync(S.rowkeep.p, 1, S.G.m, S.stream));
+    }
+    HIP_CHECK(hipStreamSynchronize(S.stream));
 }
 
 bool scaling_stale(const System& S, int precond) { return S.rs_dirty || S.cs_mode != precond; }

@@ -517,7 +517,8 @@ void ensure_sell(System& S);                    // assembled A / AT (lazy when S
 void refresh_scaling(System& S, int precond);
 // band.hip: sqrt(diag((AᵀA)⁻¹)) and op-row variances from a banded Cholesky + Takahashi inverse
 void band_factor(System& S, const int32_t* perm, BandFactor& F, int64_t nw = -1);   // nw ≥ 0: a column window
-void graph_cache_drop(const System* S);   // lsqr.hip: captured iteration batches of S
+void graph_cache_drop(const System* S);
+void upload_row_mask(System& S, const uint8_t* keep);   // build.hip: rowkeep ← keep (non-zero → 1)   // lsqr.hip: captured iteration batches of S
 void band_solve_scratch(System& S);
 void band_precond(System& S);   // S.band from S.band_order (precond 5)
 void band_launch_bsub(System& S, const double* v, int scale_mode, double* out);

@@ -110,7 +110,10 @@ class FitSystem:
             self._w_last = row_weight
         dk = np.asarray(data_keep, dtype=bool)
         if getattr(self, '_keep_last', None) is None or not np.array_equal(dk, self._keep_last):
-            self.solver.set_row_mask(np.concatenate([dk, np.ones(self.n_con, dtype=bool)]))
+            if getattr(self, '_mask', None) is None:   # constraint rows always kept: filled once
+                self._mask = np.ones(self.n_data + self.n_con, dtype=bool)
+            self._mask[:self.n_data] = dk
+            self.solver.set_row_mask(self._mask)
             self._keep_last = dk.copy()
         x, self.stats = self.solver.solve(rhs, x0=x0, b_rows=getattr(self, 'b_rows', 0), **opts)
         return x

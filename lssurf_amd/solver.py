@@ -97,7 +97,9 @@ class LSQSolver:
         self._check(self._L.lsq_set_row_weight(self._h, ptr(w)), 'lsq_set_row_weight')
 
     def set_row_mask(self, keep):
-        k = None if keep is None else as_c(np.asarray(keep, dtype=bool), np.uint8)
+        # a bool array is passed as its bytes (0/1: no copy); any non-zero byte keeps the row
+        k = None if keep is None else (keep.view(np.uint8) if isinstance(keep, np.ndarray) and keep.dtype == bool
+                                       and keep.flags.c_contiguous else as_c(np.asarray(keep, dtype=bool), np.uint8))
         self._check(self._L.lsq_set_row_mask(self._h, ptr(k)), 'lsq_set_row_mask')
 
     def set_column_blocks(self, blocks):
