@@ -685,6 +685,7 @@ struct GraphCache {
 };
 thread_local GraphCache g_cache;
 thread_local GraphCache g_cache_cg;   // CGNR iteration batches (lsqr_cg.inc)
+thread_local GraphCache g_cache_group;   // a one-rank RCCL group's CGNR batches (lsqr_cg_dist.inc)
 
 void launch_any(System& S, const Grids& g, int p, int precond, bool mf) {
     if (mf)
@@ -796,7 +797,7 @@ void prepare(System& S, int precond, bool mf) {
 }  // namespace
 
 void graph_cache_drop(const System* S) {
-    for (GraphCache* c : {&g_cache, &g_cache_cg})
+    for (GraphCache* c : {&g_cache, &g_cache_cg, &g_cache_group})
         if (c->sys == S && c->exec) {
             (void)hipGraphExecDestroy(c->exec);
             *c = GraphCache{};

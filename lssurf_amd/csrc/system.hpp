@@ -356,7 +356,8 @@ struct System {
     DBuf<int32_t> blk_cols;         // compact ids
     DBuf<int32_t> blk_full;         // full ids (stencil operator v-space)
     DBuf<double> blk_Ri;
-    DBuf<double> blk_tab;           // lazily formed systems: the block-diagonal stencil class tables (block.hip)
+    DBuf<double> blk_tab;
+    bool dist_graph_failed = false;   // a rank's batch capture was refused once: eager from then on           // lazily formed systems: the block-diagonal stencil class tables (block.hip)
     DBuf<lf_t> blk_Lf;              // R_b⁻¹ as CGNR streams it (lf_t, packed upper, block stride lf_stride(npk))
     DBuf<double> blk_tmp;           // structured ranks: block partial sums by column (kmax × n_full) for the halo
     bool blk_valid = false;
