@@ -1,4 +1,4 @@
-"""Parity at the headline size (BASELINE config C4: 1024²×12 grid, 2 M points, 12.6 M unknowns)
+"""Parity at the BASELINE sizes (C4: 1024²×12 grid, 2 M points, 12.6 M unknowns; C5: 2048²×12, 8 M points)
 through size-independent properties — the oracle cannot run here, so each property is one the
 exact answer must have:
   * the fused normal operator equals Gᵀ(w²∘(G p)) formed through the explicitly assembled CSR
@@ -96,3 +96,39 @@ def test_c4_data_colsum_against_assembled_csr(gpu_available, c4):
     got = cf[fs.keep_cols]
     assert np.linalg.norm(got - ref) <= 1e-12 * np.linalg.norm(ref)
     assert np.linalg.norm(cfg - (cf + cg)) <= 1e-12 * np.linalg.norm(cfg)
+
+
+@pytest.fixture(scope='module')
+def c5a():
+    from lssurf_amd import synthetic
+    from lssurf_amd.smooth_fit import FitSystem
+    S, _ = synthetic.aniso_system('c5a')
+    fs = FitSystem(S['G_data'], S['Gc'], S['keep'], S['Gc'].col_N, grids=S['grids'])
+    fs.solver.set_row_weight(S['w'])
+    fs.solver.set_row_mask(np.ones(S['w'].size, bool))
+    yield fs, S['w'], S['rhs']
+    fs.close()
+
+
+def test_c5a_normal_operator_and_solvers(gpu_available, c5a):
+    """BASELINE C5 (2048²×12, 8 M points, 50 M unknowns, field-valued anisotropic z0 constraints):
+    the normal operator against the assembled CSR, and the multigrid and block-Jacobi solutions
+    agreeing and satisfying the normal equations."""
+    fs, w, rhs = c5a
+    rng = np.random.default_rng(53)
+    u = np.zeros(fs.n_full)
+    u[fs.keep_cols] = rng.standard_normal(fs.keep_cols.size)
+    qu = fs.solver.normal_apply(u)
+    ref = _normal_ref(fs, w, u[fs.keep_cols])
+    assert np.linalg.norm(qu[fs.keep_cols] - ref) <= 1e-12 * np.linalg.norm(ref)
+    anorm = _anorm2(fs)
+    b = w * rhs
+    xs = {}
+    for name, opts in (('mg', dict(precond=4, method=1)), ('bj', dict(precond=3, method=1))):
+        x, st = fs.solver.solve(rhs, atol=1e-10, btol=1e-10, conlim=1e8, b_rows=fs.n_data, **opts)
+        assert st['istop'] in (1, 2), (name, st)
+        xs[name] = x
+        r = b - w * fs.solver.spmv(x)
+        ratio = np.linalg.norm(fs.solver.spmv(w * r, trans=True)) / (anorm * np.linalg.norm(r))
+        assert ratio <= 1e-7, (name, ratio)
+    assert np.linalg.norm(xs['bj'] - xs['mg']) <= 1e-7 * np.linalg.norm(xs['mg'])
