@@ -71,7 +71,7 @@ def setup_smoothness_constraints(grids, constraint_op_list, E_RMS, mask_scale, s
         op.expected = np.zeros(op.N_eq) + E_RMS['lagrangian_dzdx'] / root
         constraint_op_list.append(op)
     for op in constraint_op_list:
-        if np.any(op.expected == 0):
+        if not np.all(op.expected):   # no boolean temporary of the op's rows
             raise ValueError(f'found zero value in the expected values for {op.name}')
 
 

@@ -171,8 +171,9 @@ def _solve_opts(args, n, has_blocks=False, multigrid=False, dense_ok=True):
                 method=meth)
 
 
-def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grids, sigma_extra_masks=None):
-    """Outer editing loop (smooth_fit.py:100-210) around the device solve."""
+def iterate_fit(data, system, rhs, TCinv, G_data, Gc, in_TSE, timing, args, grids, sigma_extra_masks=None):
+    """Outer editing loop (smooth_fit.py:100-210) around the device solve.  TCinv: the diagonal of
+    the reference's TCinv (1/σ per row of [G_data; Gc])."""
     in_TSE_original = np.zeros(data.shape, dtype=bool)
     in_TSE_original[in_TSE] = True
     N_editable = np.sum(data.editable) if 'editable' in data.fields else data.size
@@ -182,17 +183,17 @@ def iterate_fit(data, system, rhs, E_all, G_data, Gc, in_TSE, timing, args, grid
     x = None
     rs_data = None
     timing['lsq_iters'] = 0
-    weight0 = np.square(E_all)             # TCinv diagonal 1/sqrt(E²), smooth_fit.py:129 (in place: 75 M rows)
-    np.sqrt(weight0, out=weight0)
-    np.divide(1., weight0, out=weight0)
+    # row weights 1/sqrt(E_all²) with E_all = 1/TCinv (smooth_fit.py:103, 129): |TCinv| — the caller's
+    # array itself when positive (no pass over, or copy of, the 77 M rows at C4)
+    weight0 = TCinv if TCinv.min() > 0 else np.abs(TCinv)
     for iteration in range(args['max_iterations']):
         weight = weight0
         if last_iteration and args['sigma_extra_relax']:
             if args['VERBOSE']:
                 print('smooth_fit.iterate_fit: relaxing errors by sigma_extra')
-            E2_plus = E_all ** 2
-            E2_plus[0:G_data.shape[0]] += sigma_extra ** 2
-            weight = 1. / np.sqrt(E2_plus)
+            nd = G_data.shape[0]   # E2_plus = E_all² + sigma_extra² on the data rows only
+            weight = weight0.copy()
+            weight[:nd] = 1. / np.sqrt((1. / TCinv[:nd]) ** 2 + sigma_extra ** 2)
         if args['VERBOSE']:
             print('starting device lsqr solve for iteration %d at %s' % (iteration, ctime()), flush=True)
         tic = time()
@@ -322,6 +323,31 @@ def _device_constraint_stats(system, m0, Gc, R, RMS):
     return True
 
 
+def tcinv_diagonal(Ed, Gc, constraint_op_list):
+    """The diagonal of TCinv = diag(1 / [Ed; Ec]) (smooth_fit.py:594-613), written in one pass from
+    the ops' expected values (no Ec, no concatenation of the 77 M rows at C4); equal bit for bit to
+    1 / np.concatenate((Ed, Ec)).  A constraint row that no op covers has Ec = 0 there: the
+    reference's zero check (the ops' own expected values were checked by
+    setup_smoothness_constraints)."""
+    nd = Ed.size
+    out = np.empty(nd + Gc.N_eq)
+    np.divide(1., Ed, out=out[:nd])
+    Tc = out[nd:]
+    covered = 0
+    for op in constraint_op_list:
+        rows = _toc_slice(Gc, op.name)
+        e = np.ravel(op.expected)
+        if isinstance(rows, slice):
+            np.divide(1., e, out=Tc[rows])
+            covered += rows.stop - rows.start
+        else:
+            Tc[rows] = 1. / e
+            covered += np.size(rows)
+    if covered != Gc.N_eq:
+        raise ValueError('zero value found in constraint sigma')
+    return out
+
+
 def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args, ru=None, system=None):
     """Output grids and fit statistics (smooth_fit.py:276-352).  With the device `system` the
     constraint statistics and the count / misfit maps are reduced on the device."""
@@ -340,6 +366,8 @@ def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args,
     m['sensor_bias_grids'] = {}
     m['jitter_bias_grids'] = {}
     if system is None or not _device_constraint_stats(system, m0, Gc, R, RMS):
+        if callable(Ec):         # smooth_fit's on-demand constraint sigma
+            Ec = Ec()
         if ru is None:           # unscaled constraint residuals Gc·m0 (device product when available)
             ru = system.solver.spmv(m0[system.keep_cols])[system.n_data:] if hasattr(system, 'solver') \
                 else Gc.toCSR().dot(m0)
@@ -449,18 +477,18 @@ def smooth_fit(**kwargs):
             zero_prior.add(op.name)
     Gc = lin_op(None, name='constraints').vstack(constraint_op_list)
     N_eq = G_data.N_eq + Gc.N_eq
-    Ec = np.zeros(Gc.N_eq)
-    for op in constraint_op_list:
-        Ec[_toc_slice(Gc, op.name)] = op.expected
     Ed = data.sigma.ravel()
-    if np.any(Ed == 0):
+    if not np.all(Ed):     # no boolean temporary
         raise ValueError('zero value found in data sigma')
-    if np.any(Ec == 0):
-        raise ValueError('zero value found in constraint sigma')
+    TCinv_diag = tcinv_diagonal(Ed, Gc, constraint_op_list)
+
+    def Ec():   # the reference reads Ec only as 1/Ec: made on demand (73 M rows at C4)
+        out = np.zeros(Gc.N_eq)
+        for op in constraint_op_list:
+            out[_toc_slice(Gc, op.name)] = op.expected
+        return out
     if args['DEBUG']:
         print_TOC(G_data, Gc)
-    TCinv_diag = np.concatenate((Ed, Ec))
-    np.divide(1., TCinv_diag, out=TCinv_diag)
     rhs = np.zeros([N_eq])
     rhs[0:data.size] = data.z.ravel()
     b_rows = data.size   # rhs[b_rows:] == 0: only the data rows (and non-zero priors) cross PCIe
@@ -482,7 +510,7 @@ def smooth_fit(**kwargs):
     if args['VERBOSE']:
         print('initial: %d:' % np.max(G_data.r), flush=True)
     if args['return_fit_objects']:
-        return {'data': data, 'G_data': G_data, 'Gc': Gc, 'grids': grids, 'Ed': Ed, 'Ec': Ec}
+        return {'data': data, 'G_data': G_data, 'Gc': Gc, 'grids': grids, 'Ed': Ed, 'Ec': Ec()}
 
     system = None
     try:
@@ -502,7 +530,7 @@ def smooth_fit(**kwargs):
             system.b_rows = b_rows
             timing['device_setup'] = time() - tic
             tic_iteration = time()
-            m0, sigma_extra, in_TSE, rs_data = iterate_fit(data, system, rhs, 1. / TCinv_diag, G_data, Gc, in_TSE,
+            m0, sigma_extra, in_TSE, rs_data = iterate_fit(data, system, rhs, TCinv_diag, G_data, Gc, in_TSE,
                                                            timing, args, grids,
                                                            sigma_extra_masks=args['sigma_extra_masks'])
             timing['iteration'] = time() - tic_iteration
@@ -512,7 +540,7 @@ def smooth_fit(**kwargs):
             data.assign({'z_est': np.reshape(system.data_forward(m0[keep_cols]), data.shape)})
             if args['mask_update_function'] is not None:
                 averaging_ops = {}
-                parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args)
+                parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec(), grids, args)
                 args['mask_update_function'](grids, m, args)
             averaging_ops = setup_averaging_ops(grids['dz'], grids['dz'].col_N, args, grids['dz'].cell_area)
             averaging_ops.update(setup_z0_avg(grids, grids['dz'].col_N, args))
@@ -536,7 +564,7 @@ def smooth_fit(**kwargs):
             if args['VERBOSE']:
                 print('Starting uncertainty calculation', flush=True)
                 tic_error = time()
-            calc_and_parse_errors(E, G_data, Gc, Ed, Ec, data, in_TSE, keep_cols, grids, averaging_ops,
+            calc_and_parse_errors(E, G_data, Gc, Ed, Ec(), data, in_TSE, keep_cols, grids, averaging_ops,
                                   device=args['device'], timing=timing, method=args['lsq_E_method'])
             if args['VERBOSE']:
                 print('\tUncertainty propagation took %3.2f seconds' % (time() - tic_error), flush=True)
