@@ -352,10 +352,12 @@ def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args,
     """Output grids and fit statistics (smooth_fit.py:276-352).  With the device `system` the
     constraint statistics and the count / misfit maps are reduced on the device."""
     z0g, dzg = grids['z0'], grids['dz']
+    # the column ranges as slices (a copy of a slice, not a 12 M-entry gather at C4)
+    cols_of = {ff: _as_slice(G_data.TOC['cols'][ff]) for ff in ('z0', 'dz')}
     m['z0'] = pc.grid.data().from_dict({'x': z0g.ctrs[1], 'y': z0g.ctrs[0], 'cell_area': z0g.cell_area,
-                                        'mask': z0g.mask, 'z0': np.reshape(m0[G_data.TOC['cols']['z0']], z0g.shape)})
+                                        'mask': z0g.mask, 'z0': np.reshape(np.array(m0[cols_of['z0']]), z0g.shape)})
     m['dz'] = pc.grid.data().from_dict({'x': dzg.ctrs[1], 'y': dzg.ctrs[0], 'time': dzg.ctrs[2],
-                                        'dz': np.reshape(m0[G_data.TOC['cols']['dz']], dzg.shape),
+                                        'dz': np.reshape(np.array(m0[cols_of['dz']]), dzg.shape),
                                         'cell_area': dzg.cell_area, 'mask': dzg.mask})
     for key, op in averaging_ops.items():
         fields = {coord: ctr for coord, ctr in zip(op.dst_grid.coords, op.dst_grid.ctrs)}
@@ -413,7 +415,7 @@ def parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec, grids, args,
         for key, vals in per_point.items():
             sums[key] = np.bincount(c_sel, weights=v_sel * vals[p_sel], minlength=n_cols)
     for ff in ['dz', 'z0']:
-        cols = G_data.TOC['cols'][ff]
+        cols = cols_of[ff]
         shape = grids[ff].shape
         m[ff].assign({'count': sums['count'][cols].reshape(shape)})
         m[ff].count[m[ff].count == 0] = np.nan
