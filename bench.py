@@ -30,6 +30,15 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def _weights_rhs(S):
+    """smooth_fit's first-iteration row weights 1/sqrt(E_all²) = |TCinv| (smooth_fit.py:103, 129;
+    lssurf_amd.smooth_fit.iterate_fit) and right-hand side, host work before device formation."""
+    w = np.abs(1. / np.concatenate((S['Ed'], S['Ec'])))
+    rhs = np.zeros(w.size)
+    rhs[:S['data'].size] = S['data'].z
+    return w, rhs
+
+
 def build_system(config, device):
     import lssurf_amd as LS
     from lssurf_amd import synthetic
@@ -53,12 +62,9 @@ def build_system(config, device):
     D, kw = synthetic.points(config)
     S = LS.smooth_fit(data=D, return_fit_objects=True, VERBOSE=False, **kw)
     keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch'])
+    w, rhs = _weights_rhs(S)
     t1 = time.time()
     fs = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, device=device, grids=S['grids'])
-    E_all = 1 / (1. / np.concatenate((S['Ed'], S['Ec'])))
-    w = 1. / np.sqrt(E_all ** 2)
-    rhs = np.zeros(w.size)
-    rhs[:S['data'].size] = S['data'].z
     fs.solver.set_row_weight(w)
     fs.solver.set_row_mask(np.ones(w.size, bool))
     t2 = time.time()
@@ -77,12 +83,9 @@ def build_dist_system(config, rank, world, device):
     D, kw = synthetic.points(config)
     S = LS.smooth_fit(data=D, return_fit_objects=True, VERBOSE=False, **kw)
     keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch'])
+    w, rhs = _weights_rhs(S)
     t1 = time.time()
     ds = DistFitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, rank, world, device)
-    E_all = 1 / (1. / np.concatenate((S['Ed'], S['Ec'])))
-    w = 1. / np.sqrt(E_all ** 2)
-    rhs = np.zeros(w.size)
-    rhs[:S['data'].size] = S['data'].z
     ds.iterate(w, rhs, 1)       # uploads weights / local rhs, builds the scaling and workspace
     t2 = time.time()
     return ds, rhs, w, {'host_assembly_s': t1 - t0, 'device_formation_s': t2 - t1}
