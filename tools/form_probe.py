@@ -9,7 +9,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main(cfg):
+def main(cfg, reps=1):
     import lssurf_amd as LS
     from lssurf_amd import synthetic
     from lssurf_amd.constraint_functions import reference_epoch_keep_cols
@@ -41,10 +41,19 @@ def main(cfg):
     tic = time.time()
     sol.set_column_blocks_csr(*blocks)
     tm['set_column_blocks'] = time.time() - tic
+    import numpy as np
+    w = np.abs(1. / np.concatenate((S['Ed'], S['Ec'])))
+    tic = time.time()
+    sol.set_row_weight(w)
+    tm['set_row_weight'] = time.time() - tic
+    tic = time.time()
+    sol.set_row_mask(np.ones(w.size, bool))
+    tm['set_row_mask'] = time.time() - tic
     t2 = time.time()
     print(json.dumps({'config': cfg, 'host_assembly_s': t1 - t0, 'formation_s': t2 - t1, 'steps': tm}), flush=True)
     sol.close()
 
 
 if __name__ == '__main__':
-    main(sys.argv[1] if len(sys.argv) > 1 else 'c4')
+    for _ in range(int(sys.argv[2]) if len(sys.argv) > 2 else 1):
+        main(sys.argv[1] if len(sys.argv) > 1 else 'c4')

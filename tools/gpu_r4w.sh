@@ -1,6 +1,6 @@
 # round 4, session w (development): the multigrid per-solve set-up (≤ 15 ms at C4) —
 # fewer power steps per level (LSQ_MG_POW) and one more level above a smaller dense coarsest
-# (LSQ_MG_COARSE 5: ≤ 5 nodes per side instead of 9), at C4, C5a and C3
+# (LSQ_MG_COARSE 5: ≤ 5 nodes per side instead of 9), at C4, C5a and C3; the formation steps at C4
 set -uo pipefail
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r4w}
 mkdir -p $OUT
@@ -13,3 +13,5 @@ for v in "LSQ_MG_POW=10" "LSQ_MG_POW=6" "LSQ_MG_POW=7" "LSQ_MG_COARSE=5" "LSQ_MG
   python3 -c "import json; d=json.load(open('$OUT/$tag.json')); print('$cfg $v', 'setup', round(d['solve_setup_s']*1e3,2), 'ms solve', round(d['solve_time_s'],4), d['solve_iters'], 'first', round(d.get('solve_setup_first_s',0)*1e3,1))"
 done
 done
+timeout -k 10 300 python3 tools/form_probe.py c4 2 > $OUT/form_probe_c4.jsonl 2> $OUT/form_probe_c4.err || { echo "form probe failed"; tail -3 $OUT/form_probe_c4.err; exit 1; }
+cat $OUT/form_probe_c4.jsonl
