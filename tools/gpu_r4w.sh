@@ -1,11 +1,15 @@
 # round 4, session w (development): the multigrid per-solve set-up (≤ 15 ms at C4) —
 # fewer power steps per level (LSQ_MG_POW) and one more level above a smaller dense coarsest
-# (LSQ_MG_COARSE 5: ≤ 5 nodes per side instead of 9), at C4, C5a and C3; the formation steps at C4
+# (LSQ_MG_COARSE 5: ≤ 5 nodes per side instead of 9), at C4, C5a and C3, after the one-wave dense
+# tile kernels' tests; the formation steps at C4
 set -uo pipefail
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r4w}
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_lsqr.py tests/test_gpu_mg.py tests/test_gpu_smooth_fit.py tests/test_gpu_band.py tests/test_gpu_tri.py tests/test_gpu_solve_sequence.py -x -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+rc=$?; tail -2 $OUT/gpu_tests.log; grep -E "^FAILED|^ERROR|^E  " $OUT/gpu_tests.log | head -10
+[ $rc -eq 0 ] || exit 1
 for cfg in c4 c5a c3; do
 for v in "LSQ_MG_POW=10" "LSQ_MG_POW=6" "LSQ_MG_POW=7" "LSQ_MG_COARSE=5" "LSQ_MG_COARSE=5 LSQ_MG_POW=7"; do
   tag=${cfg}_$(echo $v | tr ' =' '__')
