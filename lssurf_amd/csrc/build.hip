@@ -951,6 +951,9 @@ System::~System() {
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
     if (side) (void)hipStreamDestroy(side);
+    if (ev_aux) (void)hipEventDestroy(ev_aux);
+    if (aux) (void)hipStreamDestroy(aux);
+    if (aux_side) (void)hipStreamDestroy(aux_side);
     if (stream && own_stream) (void)hipStreamDestroy(stream);
 }
 
