@@ -341,6 +341,8 @@ void set_column_blocks(System& S, int64_t nb, const int64_t* ptr, const int32_t*
     std::vector<int64_t> P;
     std::vector<int32_t> C;
     std::vector<uint8_t> seen(n, 0);
+    P.reserve((size_t)std::max<int64_t>(nb, 0) + 1);
+    C.reserve((size_t)n);
     P.push_back(0);
     int kmax = 1;
     if (nb > 0) {
