@@ -50,7 +50,7 @@ def lump_by_node(D, node, slot):
     return sp.csr_matrix((Dc.data[ok], (Dc.row[ok], jn[ok])), shape=D.shape)
 
 
-def hierarchy(A, n_data_rows, keep_cols, ny, nx, nt, coarse=9):
+def hierarchy(A, n_data_rows, keep_cols, ny, nx, nt, coarse=5):   # coarse: mg.inc MG_COARSE
     """Levels [(shape, keep_mask_full, N_operator_full)] with N over each level's FULL column
     space (rows / columns of removed epochs zero).  Level 0: AᵀA; coarse: Galerkin stencil part +
     lumped data part."""
