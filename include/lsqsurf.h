@@ -162,6 +162,16 @@ int lsq_set_row_mask(lsq_handle* h, const uint8_t* keep);
  * (lsq_dist_set_halo) the blocks are the rank's owned nodes in its local compact ids, factored
  * from the rank's own rows; ghost columns stay outside every block. */
 int lsq_set_column_blocks(lsq_handle* h, int64_t n_blocks, const int64_t* block_ptr, const int32_t* cols);
+/* The same blocks given by their affine structure, as smooth_fit's node blocks are (single-GPU
+ * handles): block b (0 <= b < n_blocks) holds the k <= 16 compact columns base[j] + b*stride[j],
+ * whose full columns (lsq_set_col_map) are full_base[j] + b*full_stride[j].  The blocks must cover
+ * every compact column exactly once (n_blocks*k == n).  The library forms the block arrays on the
+ * device and checks all of this there (no 10^7-entry host column lists); on a violation it
+ * returns < 0 and leaves no blocks set.  Replaces the explicit block_ptr / cols that
+ * constraint_functions.node_column_blocks builds for the reference's Ip_c column space
+ * (constraint_functions.py:112-151: every column except dz[:, :, reference_epoch]). */
+int lsq_set_column_blocks_affine(lsq_handle* h, int64_t n_blocks, int32_t k, const int64_t* base, const int64_t* stride,
+                                 const int64_t* full_base, const int64_t* full_stride);
 
 int lsq_shape(lsq_handle* h, int64_t* m, int64_t* n, int64_t* nnz);
 /* Download the formed A (selected rows only, in row order; canonical CSR, sorted columns). */

@@ -126,6 +126,37 @@ def _node_column_blocks_uniform(z0, dz, keep_cols, max_block):
     return np.arange(0, (nn + 1) * k, k, dtype=np.int64), cols.ravel()
 
 
+def node_column_blocks_affine(grids, keep_cols, max_block=16):
+    """node_column_blocks' usual case as its affine structure, for lsq_set_column_blocks_affine:
+    (n_blocks, base, stride, full_base, full_stride) with block b = the compact columns
+    base[j] + b·stride[j] (full ids full_base[j] + b·full_stride[j]) — the same blocks, in the same
+    order, as node_column_blocks.  Read from nodes 0 and 1 only (binary searches in the ascending
+    keep_cols); the library checks every node on the device.  None when the structure does not
+    apply (then node_column_blocks)."""
+    z0, dz = grids.get('z0'), grids.get('dz')
+    if dz is None or dz.N_dims != 3:
+        return None
+    keep_cols = np.asarray(keep_cols)
+    ny, nx, nt = (int(s) for s in dz.shape)
+    nn = ny * nx
+    if nn < 2 or keep_cols.size == 0:
+        return None
+    same = z0 is not None and tuple(z0.shape) == (ny, nx) and all(
+        np.array_equal(a, b) for a, b in zip(z0.ctrs, dz.ctrs[:2]))
+    fstride = ([1] if same else []) + [nt] * nt
+    full0 = np.array(([int(z0.col_0)] if same else []) + [int(dz.col_0) + t for t in range(nt)], dtype=np.int64)
+    full1 = full0 + np.array(fstride, dtype=np.int64)
+    pos0, pos1 = np.searchsorted(keep_cols, full0), np.searchsorted(keep_cols, full1)
+    kept0 = (pos0 < keep_cols.size) & (keep_cols[np.minimum(pos0, keep_cols.size - 1)] == full0)
+    kept1 = (pos1 < keep_cols.size) & (keep_cols[np.minimum(pos1, keep_cols.size - 1)] == full1)
+    k = int(kept0.sum())
+    if not np.array_equal(kept0, kept1) or k == 0 or k > max_block or nn * k != keep_cols.size:
+        return None
+    base = pos0[kept0].astype(np.int64)
+    return (nn, base, pos1[kept0].astype(np.int64) - base, full0[kept0],
+            np.array(fstride, dtype=np.int64)[kept0])
+
+
 def node_column_blocks(grids, keep_cols, max_block=16):
     """Column blocks of the block-Jacobi preconditioner (lsq precond 3):
     one block per (y, x) node = its z0 column (when the z0 and dz grids share the node lattice)

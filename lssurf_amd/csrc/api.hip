@@ -217,6 +217,17 @@ int lsq_set_column_blocks(lsq_handle* h, int64_t n_blocks, const int64_t* block_
     });
 }
 
+int lsq_set_column_blocks_affine(lsq_handle* h, int64_t n_blocks, int32_t k, const int64_t* base,
+                                 const int64_t* stride, const int64_t* full_base, const int64_t* full_stride) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_set_column_blocks_affine: no matrix");
+        if (S.dist) return fail(S, "lsq_set_column_blocks_affine: single-GPU handles only");
+        lsq::graph_cache_drop(&S);
+        lsq::set_column_blocks_affine(S, n_blocks, k, base, stride, full_base, full_stride);
+        return 0;
+    });
+}
+
 int lsq_set_row_mask(lsq_handle* h, const uint8_t* keep) {
     return guarded(h, [&](lsq::System& S) {
         if (!S.G.rp.p) return fail(S, "lsq_set_row_mask: no matrix");

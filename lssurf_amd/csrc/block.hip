@@ -334,7 +334,89 @@ __global__ __launch_bounds__(BLOCK) void k_full_ids(int64_t n, const int32_t* __
         out[i] = keep ? keep[cols[i]] : cols[i];
 }
 
+// affine blocks: ptr[b] = b·k; column j of block b = base_j + b·stride_j (compact), checked: in
+// range, each compact column in exactly one block (nb·k == n), full id fbase_j + b·fstride_j
+struct AffDesc {
+    int64_t base[KB], stride[KB], fbase[KB], fstride[KB];
+};
+__global__ __launch_bounds__(BLOCK) void k_affine_blocks(int64_t nb, int k, int64_t n, AffDesc a,
+                                                         const int32_t* __restrict__ keep, int64_t* __restrict__ ptr,
+                                                         int32_t* __restrict__ cols, int32_t* __restrict__ full,
+                                                         int* __restrict__ seen, int* __restrict__ err) {
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < nb * k; i += (int64_t)gridDim.x * BLOCK) {
+        const int64_t b = i / k;
+        const int j = (int)(i - b * k);
+        if (j == 0) ptr[b] = b * k;
+        if (i == 0) ptr[nb] = nb * k;
+        const int64_t c = a.base[j] + b * a.stride[j];
+        if (c < 0 || c >= n) {
+            atomicOr(err, 1);
+            cols[i] = 0;
+            full[i] = 0;
+            continue;
+        }
+        cols[i] = (int32_t)c;
+        const int64_t f = keep ? keep[c] : c;
+        full[i] = (int32_t)f;
+        if (f != a.fbase[j] + b * a.fstride[j]) atomicOr(err, 2);
+        if (atomicAdd(seen + c, 1) != 0) atomicOr(err, 4);
+    }
+}
+
 }  // namespace
+
+// Column blocks given by their affine structure (lsq_set_column_blocks_affine): the arrays of
+// set_column_blocks formed on the device, the structure checked there; no host column lists.
+void set_column_blocks_affine(System& S, int64_t nb, int k, const int64_t* base, const int64_t* stride,
+                              const int64_t* fbase, const int64_t* fstride) {
+    const int64_t n = S.G.n;
+    if (nb < 1 || k < 1 || k > KB || !base || !stride || !fbase || !fstride)
+        throw std::invalid_argument("lsq_set_column_blocks_affine: bad arguments");
+    if (nb * k != n) throw std::invalid_argument("lsq_set_column_blocks_affine: the blocks must cover every column");
+    AffDesc a{};
+    for (int j = 0; j < k; ++j) {
+        a.base[j] = base[j];
+        a.stride[j] = stride[j];
+        a.fbase[j] = fbase[j];
+        a.fstride[j] = fstride[j];
+    }
+    S.blk_ptr.alloc(nb + 1);
+    S.blk_cols.alloc(n);
+    S.blk_full.alloc(n);
+    DBuf<int> seen(n), err(1);
+    seen.zero(S.stream);
+    err.zero(S.stream);
+    hipLaunchKernelGGL(k_affine_blocks, dim3(grid_for(n)), dim3(BLOCK), 0, S.stream, nb, k, n, a,
+                       S.mf ? S.keep.p : nullptr, S.blk_ptr.p, S.blk_cols.p, S.blk_full.p, seen.p, err.p);
+    KERNEL_CHECK();
+    int e = 0;
+    err.download(&e, 1, S.stream);
+    HIP_CHECK(hipStreamSynchronize(S.stream));
+    if (e) {
+        S.nblk = 0;   // no half-formed structure left behind (precond 3 then takes singletons)
+        S.blk_kmax = 0;
+        S.blk_affine = S.blk_user = S.blk_valid = false;
+        S.blk_ptr = DBuf<int64_t>();
+        S.blk_cols = DBuf<int32_t>();
+        S.blk_full = DBuf<int32_t>();
+        S.blk_Ri = DBuf<double>();
+        S.iter_ready = false;
+        throw std::invalid_argument(e & 1 ? "lsq_set_column_blocks_affine: column out of range"
+                                    : e & 4 ? "lsq_set_column_blocks_affine: column in two blocks"
+                                            : "lsq_set_column_blocks_affine: full column ids differ from full_base / full_stride");
+    }
+    S.nblk = nb;
+    S.blk_kmax = k;
+    S.blk_affine = nb > 1;
+    for (int j = 0; j < k; ++j) {
+        S.blk_aff.base[j] = fbase[j];
+        S.blk_aff.stride[j] = fstride[j];
+    }
+    S.blk_Ri = DBuf<double>();
+    S.blk_valid = false;
+    S.blk_user = true;
+    S.iter_ready = false;
+}
 
 void set_column_blocks(System& S, int64_t nb, const int64_t* ptr, const int32_t* cols) {
     const int64_t n = S.G.n;

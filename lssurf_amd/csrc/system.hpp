@@ -543,6 +543,8 @@ void csr_rows_sumsq(System& S, const double* dx, int64_t first, int64_t count, d
 
 // block.hip
 void set_column_blocks(System& S, int64_t nb, const int64_t* ptr, const int32_t* cols);
+void set_column_blocks_affine(System& S, int64_t nb, int k, const int64_t* base, const int64_t* stride,
+                              const int64_t* fbase, const int64_t* fstride);
 void ensure_blocks(System& S);                     // default structure if none was set
 void block_factor(System& S);                      // R_b⁻¹ for the current row scale
 void block_normal(System& S);                      // (AᵀA)_bb of the system's own rows into blk_Ri

@@ -24,7 +24,8 @@ import numpy as np
 
 from . import containers as pc
 from .calc_sigma_extra import RDE, calc_sigma_extra, calc_sigma_extra_on_grid
-from .constraint_functions import build_reference_epoch_matrix, node_column_blocks, reference_epoch_keep_cols, \
+from .constraint_functions import build_reference_epoch_matrix, node_column_blocks, \
+    node_column_blocks_affine, reference_epoch_keep_cols, \
     setup_smoothness_constraints
 from .grid_functions import setup_averaging_ops, setup_avg_mask_ops, setup_grids, setup_z0_avg, \
     validate_by_dz_mask
@@ -78,15 +79,32 @@ class FitSystem:
             self.solver.set_matrix_coo(m, self.n_full, np.concatenate([r1, r2 + self.n_data]),
                                        np.concatenate([c1, c2]), np.concatenate([v1, v2]))
         self.has_blocks = False
+        self._grids, self._blocks = grids, None
         if grids is not None:      # per-node column blocks for the block-Jacobi preconditioner
-            blocks = node_column_blocks(grids, keep_cols)
-            if blocks is not None:
-                self.solver.set_column_blocks_csr(*blocks)
-                self.has_blocks = True
-                self.blocks = blocks   # (block_ptr, cols): bench.py's algorithm-matched CPU baseline
+            aff = node_column_blocks_affine(grids, keep_cols)
+            if aff is not None:    # formed and checked on the device (no 10⁷-entry host lists)
+                try:
+                    self.solver.set_column_blocks_affine(*aff)
+                    self.has_blocks = True
+                except NativeError:
+                    pass
+            if not self.has_blocks:
+                blocks = node_column_blocks(grids, keep_cols)
+                if blocks is not None:
+                    self.solver.set_column_blocks_csr(*blocks)
+                    self.has_blocks = True
+                    self._blocks = blocks
         self._mg = None            # multigrid (precond 4) availability, probed on first use
         self.mg_build_s = 0.0
         self.stats = None
+
+    @property
+    def blocks(self):
+        """(block_ptr, cols) of the node blocks (bench.py's algorithm-matched CPU baseline), made
+        on first use when the device took them in affine form."""
+        if self._blocks is None and self.has_blocks:
+            self._blocks = node_column_blocks(self._grids, self.keep_cols)
+        return self._blocks
 
     def multigrid_available(self, row_weight=None):
         """True when the geometric multigrid preconditioner (lsq precond 4) runs on this system

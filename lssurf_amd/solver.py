@@ -119,6 +119,14 @@ class LSQSolver:
         c_ = as_c(cols, np.int32)
         self._check(self._L.lsq_set_column_blocks(self._h, p_.size - 1, ptr(p_), ptr(c_)), 'lsq_set_column_blocks')
 
+    def set_column_blocks_affine(self, n_blocks, base, stride, full_base, full_stride):
+        """Blocks b < n_blocks of the compact columns base[j] + b·stride[j] with full ids
+        full_base[j] + b·full_stride[j] (lsq_set_column_blocks_affine: formed and checked on the
+        device; NativeError when the structure does not hold)."""
+        a = [as_c(np.asarray(v, dtype=np.int64), np.int64) for v in (base, stride, full_base, full_stride)]
+        self._check(self._L.lsq_set_column_blocks_affine(self._h, int(n_blocks), a[0].size, *(ptr(v) for v in a)),
+                    'lsq_set_column_blocks_affine')
+
     def shape(self):
         m, n, z = (ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64())
         self._check(self._L.lsq_shape(self._h, ctypes.byref(m), ctypes.byref(n), ctypes.byref(z)), 'lsq_shape')

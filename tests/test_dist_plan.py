@@ -254,3 +254,28 @@ def test_node_column_blocks_uniform_fast_path():
             cf._node_column_blocks_uniform = saved
         assert np.array_equal(fast[0], ref[0]) and np.array_equal(fast[1], ref[1]), name
         assert fast[1].dtype == np.int32 and fast[0].dtype == np.int64
+
+
+def test_node_column_blocks_affine_matches_explicit():
+    """The affine form of the node blocks (lsq_set_column_blocks_affine) expands to exactly
+    node_column_blocks' (block_ptr, cols); systems whose blocks leave singleton columns (z0 on a
+    2× refinement) or whose kept set is not the same at every node get None (explicit path)."""
+    from lssurf_amd import constraint_functions as cf
+    import lssurf_amd as LS
+    for name in ('t64', 't15', 't64z'):
+        D, kw = synthetic.points(name)
+        S = LS.smooth_fit(data=D, return_fit_objects=True, VERBOSE=False, **kw)
+        keep = np.asarray(cf.reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch']))
+        ref = cf.node_column_blocks(S['grids'], keep)
+        aff = cf.node_column_blocks_affine(S['grids'], keep)
+        if name == 't64z':
+            assert aff is None
+            continue
+        nb, base, stride, fbase, fstride = aff
+        b = np.arange(nb)[:, None]
+        cols = base[None, :] + b * stride[None, :]
+        np.testing.assert_array_equal(ref[0], np.arange(nb + 1) * base.size)
+        np.testing.assert_array_equal(ref[1], cols.ravel())
+        np.testing.assert_array_equal(keep[cols], fbase[None, :] + b * fstride[None, :])
+        hole = np.delete(keep, keep.size // 2)          # one node short of a column
+        assert cf.node_column_blocks_affine(S['grids'], hole) is None
