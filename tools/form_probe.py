@@ -35,14 +35,22 @@ def main(cfg, reps=1):
     sol.set_matrix_stencil(int(G_data.N_eq) + int(Gc.N_eq), n_full, gdesc, interp, coords, stencils, npts,
                            fields=fields)
     tm['set_matrix_stencil'] = time.time() - tic
+    from lssurf_amd.constraint_functions import node_column_blocks_affine
+    tic = time.time()
+    aff = node_column_blocks_affine(S['grids'], keep)
+    tm['node_column_blocks_affine'] = time.time() - tic
+    tic = time.time()
+    sol.set_column_blocks_affine(*aff)
+    tm['set_column_blocks_affine'] = time.time() - tic
     tic = time.time()
     blocks = node_column_blocks(S['grids'], keep)
-    tm['node_column_blocks'] = time.time() - tic
+    tm['node_column_blocks (explicit, for comparison)'] = time.time() - tic
     tic = time.time()
     sol.set_column_blocks_csr(*blocks)
-    tm['set_column_blocks'] = time.time() - tic
+    tm['set_column_blocks (explicit, for comparison)'] = time.time() - tic
     import numpy as np
     w = np.abs(1. / np.concatenate((S['Ed'], S['Ec'])))
+    tm['formation_affine_s'] = sum(v for k, v in tm.items() if 'explicit' not in k)
     tic = time.time()
     sol.set_row_weight(w)
     tm['set_row_weight'] = time.time() - tic
