@@ -215,7 +215,6 @@ struct CgGrid {
     // wave-strip operator (lsqr_cg_rw.inc): strips of rw_sx dim-1 positions × rw_ry rows, rw_nsx ×
     // rw_nry of them, rw_chunk per XCD; its class table (per dim-0 class) from coefc[rwc0]
     int32_t rw_sx, rw_nsx, rw_ry, rw_nry, rw_chunk, rwc0;
-    int32_t rw_cm;                           // strips numbered down the rows first (development A/B)
 };
 struct BlkAffine {
     int64_t base[16], stride[16];
