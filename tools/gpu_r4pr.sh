@@ -1,5 +1,6 @@
 # round 4 (development): the probing estimator of diag((AᵀA)⁻¹) on multigrid PCG against the band
-# covariance at t64 (64²×12) and t128 (128²×12): VERDICT r3 #8
+# covariance at t64 (64²×12) and t128 (128²×12): VERDICT r3 #8 (the D = 16 pass at t64 ran past the
+# 500 s limit — 0.18 s per probe through the host round trips — after D = 4 and 8 had reported)
 set -uo pipefail
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r4pr}
 mkdir -p $OUT
