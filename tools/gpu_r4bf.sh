@@ -1,4 +1,4 @@
-# round 4 (development): the register-resident block factor kernel — the whole -m gpu suite, smoke,
+# round 4 (development): the register-resident block factor kernel and the data-row CG start — the whole -m gpu suite, smoke,
 # then C4 / C5a / C3 multigrid set-up and solve, and the default bench
 set -uo pipefail
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r4bf}
