@@ -399,16 +399,17 @@ class lin_op:
         rows = np.flatnonzero(g.validate_pts(pts))
         if bounds_error and rows.size < len(pts[0]):
             raise ValueError(f'Found {len(pts[0]) - rows.size} points out of bounds for grid {g.name}')
-        pts = [p[rows] for p in pts]
-        fsub = g.float_sub(pts)
-        cell = g.cell_sub_for_pts(pts)
-        frac = [a - b for a, b in zip(fsub, cell)]
-        base = g.global_ind(cell)
+        if rows.size < len(pts[0]):
+            pts = [p[rows] for p in pts]
         corners = np.c_[[k.ravel() for k in np.mgrid[tuple(slice(0, 2) for _ in range(g.N_dims))]]] \
             if g.N_dims > 1 else np.array([[0, 1]])
         n_nb, npts = corners.shape[1], rows.size
 
-        def build():
+        def build():   # the triplets on first use (the device path reads only the points)
+            fsub = g.float_sub(pts)
+            cell = g.cell_sub_for_pts(pts)
+            frac = [a - b for a, b in zip(fsub, cell)]
+            base = g.global_ind(cell)
             R = np.zeros([npts, n_nb], dtype=int)
             C = np.zeros([npts, n_nb], dtype=int)
             V = np.ones([npts, n_nb], dtype=float)
