@@ -82,7 +82,7 @@ def reference_epoch_keep_cols(n_cols, dz_grid, reference_epoch):
     ref_cols = dz_grid.global_ind([iy.T.ravel(), ix.T.ravel(), np.full(iy.size, reference_epoch)])
     keep = np.ones(int(n_cols), dtype=bool)
     keep[ref_cols[(ref_cols >= 0) & (ref_cols < n_cols)]] = False
-    return np.flatnonzero(keep).astype('int')
+    return np.flatnonzero(keep).astype('int', copy=False)
 
 
 def build_reference_epoch_matrix(G_data, Gc, grids, reference_epoch, dz_mask=None):

@@ -270,8 +270,9 @@ def iterate_fit(data, system, rhs, TCinv, G_data, Gc, in_TSE, timing, args, grid
             if args['VERBOSE']:
                 print('Edited data empty, returning')
             return m0, sigma_extra, in_TSE, rs_data
-        if np.max(np.abs((m0_last - m0)[_as_slice(Gc.TOC['cols']['dz'])])) < args['converge_tol_dz'] and \
-                iteration > args['min_iterations']:
+        dsl = _as_slice(Gc.TOC['cols']['dz'])
+        ddz = np.subtract(m0_last[dsl], m0[dsl])   # max |Δdz| (smooth_fit.py:180), one temporary
+        if np.max(np.abs(ddz, out=ddz)) < args['converge_tol_dz'] and iteration > args['min_iterations']:
             if args['VERBOSE']:
                 print('Solution identical to previous iteration with tolerance %3.1f, exiting after iteration %d'
                       % (args['converge_tol_dz'], iteration))
