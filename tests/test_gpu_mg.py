@@ -248,3 +248,37 @@ def test_mg_persistent_coarse_levels(gpu_available, tmp_path):
         fs.close()
     assert abs(int(got[0]) - it) <= 1, (got[0], it)
     assert np.linalg.norm(got[1:] - x) <= 1e-8 * np.linalg.norm(x)
+
+
+_POW_CHILD = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from test_gpu_cgnr import _synthetic_system, TOL
+S, fs, w, rhs = _synthetic_system(sys.argv[3])
+try:
+    x = fs.solve(w, np.ones(fs.n_data, bool), rhs, precond=4, method=1, **TOL)
+    levels, _ = fs.solver.mg_info()
+    lam = [fs.solver.mg_apply(l, 2) for l in range(len(levels) - 1)]
+    np.save(sys.argv[2], np.concatenate([[fs.stats['iters']], lam, x]))
+finally:
+    fs.close()
+'''
+
+
+@pytest.mark.parametrize('which', ['t64', 't256'])
+def test_mg_concurrent_power_steps_match_serial(gpu_available, tmp_path, which):
+    """The per-solve set-up runs the coarse levels' power steps on a second stream pair beside
+    level 0's (each level its own vectors, scalars and partials): λ of every level and the solve
+    equal, bit for bit, a child process that runs them in turn (LSQ_MG_POW_CONC=0)."""
+    import os
+    import subprocess
+    import sys
+    got = {}
+    for conc in ('0', '1'):
+        out = tmp_path / f'x{conc}.npy'
+        env = dict(os.environ, LSQ_MG_POW_CONC=conc)
+        r = subprocess.run([sys.executable, '-c', _POW_CHILD, os.path.dirname(__file__), str(out), which], env=env,
+                           capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-2000:]
+        got[conc] = np.load(out)
+    np.testing.assert_array_equal(got['0'], got['1'])
