@@ -18,8 +18,9 @@ def main(path, which=-1):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
     k = [(short(r['Kernel_Name']), int(r['Grid_Size_X']), int(r['Start_Timestamp']), int(r['End_Timestamp'])) for r in rows]
-    # iterations of the multigrid solves: k_cg_alpha … k_cg_alpha with k_mg_ kernels between
-    starts = [i for i, e in enumerate(k) if e[0] == 'k_cg_alpha']
+    # iterations of the multigrid solves: from one k_cg_beta (the end of a CG step) to the next,
+    # with k_mg_ kernels between (α has no launch of its own since round 4's closing commit)
+    starts = [i + 1 for i, e in enumerate(k) if e[0] == 'k_cg_beta']
     its = [(a, b) for a, b in zip(starts, starts[1:]) if any(e[0].startswith('k_mg_') for e in k[a:b])
            and max(e[3] - e[2] for e in k[a:b] if e[0].startswith('k_cg_normal')) > 30_000   # live (not stopped)
            and not any(e[0] in ('k_block_factor', 'k_mg_power_scalar') for e in k[a:b])]     # no per-solve set-up
