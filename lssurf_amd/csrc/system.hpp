@@ -380,7 +380,6 @@ struct System {
     bool own_stream = true;
     hipStream_t side = nullptr;              // CGNR: k_cg_xedge beside the data kernel (fork/join events)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    DBuf<unsigned> cg_bcnt;                   // k_cg_block's arrival counter (β in its last workgroup)
     hipStream_t aux = nullptr, aux_side = nullptr;   // multigrid set-up: coarse power steps beside level 0's
     hipEvent_t ev_aux = nullptr;
     int rank = 0, nranks = 1;
