@@ -303,6 +303,25 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    def gather(obj):   # every rank's object, in rank order (gloo; set-up / reporting only)
+        if dist is None:
+            return [obj]
+        out = [None] * world
+        dist.all_gather_object(out, obj)
+        return out
+
+    ranks = None
+    if world > 1 or args.dist:
+        # self-check of a multi-GPU run: what each rank's RCCL communicator and device
+        # report; the run fails unless RCCL sees all N ranks and (without --same-device) every rank
+        # drives a card of its own
+        ranks = gather(dict(fs.comm_info(), rank=rank))
+        bad = [r for r in ranks if r['comm_count'] != world]
+        cards = [r['pci'] for r in ranks]
+        if bad or (not args.same_device and len(set(cards)) != len(cards)):
+            log(f'bench: multi-GPU self-check failed: {ranks}')
+            raise SystemExit(3)
+
     solver.iterate(rhs, args.warmup, op=args.op, precond=args.precond, method=meth)
     barrier()
     t0 = time.perf_counter()
@@ -316,6 +335,9 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_wall = float(tt[0])
 
+    if ranks is not None:   # per-rank device time of the timed iterations
+        for r, t in zip(ranks, gather(1e3 * st['time_s'] / args.steps)):
+            r['iter_ms_device'] = t
     ms_per_step = 1e3 * t_wall / args.steps
     value = args.steps / t_wall   # LSQR iterations of the ONE (row-partitioned) system per second
     Z, m, n = info['nnz'], info['m'], info['n']      # this rank's (local) system
@@ -392,6 +414,9 @@ def main():
             solve['lsqr_iters_per_s'] = solve['solve_lsqr']['solve_iters_per_s']
             solve['solve_rel_diff_vs_lsqr'] = float(np.linalg.norm(x - xl) / np.linalg.norm(xl))
 
+    if ranks is not None and solve:   # per-rank bytes sent per iteration of the full solve
+        for r, b in zip(ranks, gather(solve['solve_comm_bytes_per_iter'])):
+            r['solve_comm_bytes_per_iter'] = b
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not args.dist:
         threads = min(os.cpu_count() or 1, 16)
@@ -436,6 +461,10 @@ def main():
             'cpu_baseline': cpu,
             **solve, **setup,
         }
+        if ranks is not None:
+            its = [r['iter_ms_device'] for r in ranks]
+            out['ranks'] = ranks
+            out['rank_iter_ms_device'] = {'max': max(its), 'min': min(its)}
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

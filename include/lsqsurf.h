@@ -69,6 +69,13 @@ typedef struct lsq_opts {
     int64_t b_rows;        /* rows of b that may be non-zero: b[0, b_rows) is uploaded, the     */
                            /*     rest taken as zero (smooth_fit: the data rows, when no prior  */
                            /*     is non-zero); 0 = all m rows                                 */
+    double  anorm0;        /* CGNR: an ‖A‖ estimate to start the stopping rule from — lsq_stats */
+                           /*     .anorm of an earlier solve of the same operator and           */
+                           /*     preconditioner (smooth_fit's later outer solves, warm         */
+                           /*     starts).  The rule uses max(anorm0, the running Lanczos       */
+                           /*     estimate), which only grows towards the true norm; without it */
+                           /*     a re-solve from the solution iterates until the estimate has  */
+                           /*     rebuilt.  0 = none (scipy's rule); ignored by LSQR            */
 } lsq_opts;
 
 /* Statistics (mirrors scipy's lsqr return tuple, plus timing and the byte model). */
@@ -266,6 +273,11 @@ int lsq_band_factor(lsq_handle* h, const int32_t* perm, int64_t* info, double* R
  * columns (length n_own). */
 int lsq_dist_unique_id(uint8_t* id128);
 lsq_handle* lsq_create_dist(int32_t device, int32_t rank, int32_t nranks, const uint8_t* id128);
+/* What the rank's RCCL communicator and device report (bench.py's self-check of a multi-GPU run):
+ * out[0] ncclCommCount, out[1] ncclCommUserRank, out[2] ncclCommCuDevice, out[3] the handle's
+ * HIP device, out[4..6] its PCI domain / bus / device ids (a physical card: two ranks with equal
+ * ids share one GPU).  A handle without a communicator reports count 0. */
+int lsq_dist_comm_info(lsq_handle* h, int64_t* out7);
 int lsq_dist_referenced_cols(lsq_handle* h, uint8_t* flags);
 int lsq_dist_set_layout(lsq_handle* h, const int32_t* col_local, int64_t n_local, int64_t n_own,
                         int32_t n_peers, const int32_t* peers, const int64_t* send_cnt,

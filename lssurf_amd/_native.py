@@ -22,7 +22,8 @@ class LsqOpts(ctypes.Structure):
     _fields_ = [('method', ctypes.c_int32), ('precond', ctypes.c_int32), ('atol', ctypes.c_double),
                 ('btol', ctypes.c_double), ('conlim', ctypes.c_double), ('maxit', ctypes.c_int64),
                 ('use_x0', ctypes.c_int32), ('batch', ctypes.c_int32), ('use_graph', ctypes.c_int32),
-                ('op', ctypes.c_int32), ('b_rows', ctypes.c_int64)]
+                ('op', ctypes.c_int32), ('b_rows', ctypes.c_int64),
+                ('anorm0', ctypes.c_double)]
 
 
 class GridDesc(ctypes.Structure):
@@ -53,7 +54,7 @@ EXPORTS = ['lsq_default_opts', 'lsq_create', 'lsq_destroy', 'lsq_last_error', 'l
            'lsq_set_row_mask',
            'lsq_set_column_blocks', 'lsq_set_column_blocks_affine', 'lsq_shape', 'lsq_get_csr',
            'lsq_solve', 'lsq_spmv', 'lsq_spmv_rows', 'lsq_rows_sumsq', 'lsq_data_colsum', 'lsq_iterate', 'lsq_profile_kernels', 'lsq_cg_available', 'lsq_profile_cg', 'lsq_mg_info', 'lsq_mg_apply', 'lsq_normal_apply', 'lsq_sell_info', 'lsq_sigma_x', 'lsq_cov_band', 'lsq_cov_band_window', 'lsq_set_band_order', 'lsq_band_factor',
-           'lsq_get_rinv', 'lsq_dist_unique_id', 'lsq_create_dist', 'lsq_dist_referenced_cols',
+           'lsq_get_rinv', 'lsq_dist_unique_id', 'lsq_create_dist', 'lsq_dist_comm_info', 'lsq_dist_referenced_cols',
            'lsq_dist_set_layout', 'lsq_dist_set_halo', 'lsq_dist_set_global', 'lsq_vgroup_create', 'lsq_vgroup_rank', 'lsq_vgroup_solve', 'lsq_vgroup_iterate',
            'lsq_vgroup_last_error', 'lsq_vgroup_destroy',
            'lsq_dgroup_create', 'lsq_dgroup_rank', 'lsq_dgroup_solve', 'lsq_dgroup_iterate', 'lsq_dgroup_last_error',
@@ -109,6 +110,7 @@ def load():
         'lsq_band_factor': ([P, P, P, P, P, P], ctypes.c_int),
         'lsq_dist_unique_id': ([P], ctypes.c_int),
         'lsq_create_dist': ([i32, i32, i32, P], P),
+        'lsq_dist_comm_info': ([P, P], ctypes.c_int),
         'lsq_dist_referenced_cols': ([P, P], ctypes.c_int),
         'lsq_dist_set_layout': ([P, P, i64, i64, i32, P, P, P, P], ctypes.c_int),
         'lsq_dist_set_halo': ([P, i32, P, i32, P, P, P, P, P], ctypes.c_int),

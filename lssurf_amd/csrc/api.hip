@@ -240,15 +240,8 @@ int lsq_set_row_mask(lsq_handle* h, const uint8_t* keep) {
 int lsq_shape(lsq_handle* h, int64_t* m, int64_t* n, int64_t* nnz) {
     return guarded(h, [&](lsq::System& S) {
         if (!S.G.rp.p) return fail(S, "lsq_shape: no matrix");
-        lsq::ensure_full_csr(S);
-        std::vector<int64_t> rp(S.G.m + 1);
-        std::vector<uint8_t> keep(S.G.m);
-        S.G.rp.download(rp.data(), S.G.m + 1, S.stream);
-        S.rowkeep.download(keep.data(), S.G.m, S.stream);
-        HIP_CHECK(hipStreamSynchronize(S.stream));
         int64_t mk = 0, zk = 0;
-        for (int64_t i = 0; i < S.G.m; ++i)
-            if (keep[i]) { ++mk; zk += rp[i + 1] - rp[i]; }
+        lsq::shape_counts(S, &mk, &zk);   // no full CSR formed for it
         if (m) *m = mk;
         if (n) *n = S.G.n;
         if (nnz) *nnz = zk;
@@ -445,6 +438,31 @@ lsq_handle* lsq_create_dist(int32_t device, int32_t rank, int32_t nranks, const 
     h->sys.rank = rank;
     h->sys.nranks = nranks;
     return h;
+}
+
+int lsq_dist_comm_info(lsq_handle* h, int64_t* out) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!out) return fail(S, "lsq_dist_comm_info: null output");
+        for (int k = 0; k < 7; ++k) out[k] = 0;
+        if (S.comm) {
+            int c = 0, r = 0, d = 0;
+            if (ncclCommCount(S.comm, &c) != ncclSuccess || ncclCommUserRank(S.comm, &r) != ncclSuccess ||
+                ncclCommCuDevice(S.comm, &d) != ncclSuccess)
+                return fail(S, "lsq_dist_comm_info: RCCL query failed");
+            out[0] = c;
+            out[1] = r;
+            out[2] = d;
+        }
+        out[3] = S.device;
+        int v = 0;
+        HIP_CHECK(hipDeviceGetAttribute(&v, hipDeviceAttributePciDomainID, S.device));
+        out[4] = v;
+        HIP_CHECK(hipDeviceGetAttribute(&v, hipDeviceAttributePciBusId, S.device));
+        out[5] = v;
+        HIP_CHECK(hipDeviceGetAttribute(&v, hipDeviceAttributePciDeviceId, S.device));
+        out[6] = v;
+        return 0;
+    });
 }
 
 int lsq_dist_referenced_cols(lsq_handle* h, uint8_t* flags) {

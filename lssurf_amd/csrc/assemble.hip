@@ -50,7 +50,12 @@ __global__ __launch_bounds__(BLOCK) void k_gen_rows(int pass, const GenCtx* __re
                                                     const double* __restrict__ pt, const int32_t* __restrict__ colmap,
                                                     int64_t* __restrict__ cnt, const int64_t* __restrict__ rp,
                                                     int32_t* __restrict__ ci, double* __restrict__ val,
-                                                    unsigned long long* __restrict__ err, int64_t m) {
+                                                    unsigned long long* __restrict__ err, int64_t m,
+                                                    const uint8_t* __restrict__ keep = nullptr,
+                                                    unsigned long long* __restrict__ ksum = nullptr) {
+    // ksum (count pass, lsq_shape of a lazily formed system): instead of cnt, the kept rows and
+    // their entries are summed into ksum[0], ksum[1] (keep[r] != 0: row r kept)
+    double kr = 0.0, kz = 0.0;
     for (int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x; r < m; r += (int64_t)gridDim.x * BLOCK) {
         int64_t cols[MAXE];
         double vals[MAXE];
@@ -152,7 +157,22 @@ __global__ __launch_bounds__(BLOCK) void k_gen_rows(int pass, const GenCtx* __re
             }
             i = k;
         }
-        if (!pass) cnt[r] = out;
+        if (ksum) {
+            if (keep[r]) {
+                kr += 1.0;
+                kz += (double)out;
+            }
+        } else if (!pass) {
+            cnt[r] = out;
+        }
+    }
+    if (ksum) {   // exact: every partial count is far below 2^53
+        kr = wave_sum(kr);
+        kz = wave_sum(kz);
+        if ((threadIdx.x & 63) == 0 && kr > 0.0) {
+            atomicAdd(ksum, (unsigned long long)kr);
+            atomicAdd(ksum + 1, (unsigned long long)kz);
+        }
     }
 }
 
@@ -511,6 +531,43 @@ void ensure_full_csr(System& S) {
 }
 
 int64_t stored_rows(const System& S) { return S.g_full ? S.G.m : S.mfh.npts; }
+
+// Kept rows and their entries of the formed operator (lsq_shape).  A lazily formed system is not
+// formed for it: the row generator's count pass runs again over every row, reduced on the device
+// against the row mask (shape() used to form and keep the full G / GT).
+void shape_counts(System& S, int64_t* mk, int64_t* zk) {
+    hipStream_t strm = S.stream;
+    const int64_t m = S.G.m;
+    if (S.g_full) {
+        std::vector<int64_t> rp(m + 1);
+        std::vector<uint8_t> keep(m);
+        S.G.rp.download(rp.data(), m + 1, strm);
+        S.rowkeep.download(keep.data(), m, strm);
+        HIP_CHECK(hipStreamSynchronize(strm));
+        int64_t a = 0, z = 0;
+        for (int64_t i = 0; i < m; ++i)
+            if (keep[i]) { ++a; z += rp[i + 1] - rp[i]; }
+        *mk = a;
+        *zk = z;
+        return;
+    }
+    const GenCtx& h = *reinterpret_cast<const GenCtx*>(S.gen_ctx.data());
+    DBuf<GenCtx> dctx(1);
+    HIP_CHECK(hipMemcpyAsync(dctx.p, &h, sizeof(GenCtx), hipMemcpyHostToDevice, strm));
+    DBuf<unsigned long long> err(1), ks(2);
+    err.zero(strm);
+    ks.zero(strm);
+    const int32_t* cmap = S.have_colmap ? S.colmap.p : nullptr;
+    hipLaunchKernelGGL(k_gen_rows, dim3(grid_for(m)), dim3(BLOCK), 0, strm, 0, dctx.p, S.gen_py.p, S.gen_px.p,
+                       S.gen_pt.n ? S.gen_pt.p : nullptr, cmap, nullptr, nullptr, nullptr, nullptr, err.p, m,
+                       S.rowkeep.p, ks.p);
+    KERNEL_CHECK();
+    unsigned long long v[2] = {0, 0};
+    ks.download(v, 2, strm);
+    HIP_CHECK(hipStreamSynchronize(strm));
+    *mk = (int64_t)v[0];
+    *zk = (int64_t)v[1];
+}
 
 // z0 (gz) on a 2× refinement of the dz (g3) lattice: the points sorted by dz cell with their dz
 // subscripts — the data rows of the system Galerkin-projected onto the dz lattice (z0's bilinear

@@ -166,7 +166,8 @@ __global__ __launch_bounds__(BLOCK) void k_block_normal_tab(int64_t nb, int kmax
                                                             const int32_t* __restrict__ tci,
                                                             const double* __restrict__ tval,
                                                             const double* __restrict__ rs, BnDesc D,
-                                                            const double* __restrict__ coef, double* __restrict__ N) {
+                                                            const double* __restrict__ coef, double* __restrict__ N,
+                                                            int* __restrict__ cross) {
     const int npk = kmax * (kmax + 1) / 2;
     const int64_t total = nb * npk;
     for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < total; q += (int64_t)gridDim.x * BLOCK) {
@@ -189,7 +190,10 @@ __global__ __launch_bounds__(BLOCK) void k_block_normal_tab(int64_t nb, int kmax
             if (fj < G.col0 || fj >= G.col0 + G.nodes) break;
             const uint32_t ri = (uint32_t)(fi - G.col0), rj = (uint32_t)(fj - G.col0);
             const uint32_t ni = bn_div(ri, G.fd2), nj = bn_div(rj, G.fd2);   // (y, x) node
-            if (ni != nj) break;
+            if (ni != nj) {   // a block spanning two nodes of one grid: the tables miss their coupling
+                atomicOr(cross, 1);
+                break;
+            }
             const int ti = (int)(ri - ni * (uint32_t)G.S[2]), dt = (int)(rj - nj * (uint32_t)G.S[2]) - ti;
             const uint32_t y = bn_div(ri, G.fd1);
             const int x = (int)(ni - y * (uint32_t)G.S[1]);
@@ -558,12 +562,25 @@ void block_normal(System& S) {
     BnDesc bd;
     std::vector<double> tab;
     const bool tab_env = !(getenv("LSQ_BLK_TAB") && getenv("LSQ_BLK_TAB")[0] == '0');   // A/B + parity test (per call)
-    if (!S.g_full && tab_env && block_normal_tables(S.mfh, bd, tab)) {   // lazily formed, class tables
+    // lazily formed, class tables: they hold the stencil terms between columns of ONE (y, x) node
+    // only, so a block that pairs two nodes of one grid (a user block set by lsq_set_column_blocks)
+    // is flagged by the kernel and the block normals are redone by the part-descriptor kernel
+    bool tab_done = false;
+    if (!S.g_full && tab_env && block_normal_tables(S.mfh, bd, tab)) {
         S.blk_tab.alloc(std::max<int64_t>((int64_t)tab.size(), 1));
         S.blk_tab.upload(tab.data(), (int64_t)tab.size(), S.stream);
+        DBuf<int> cross(1);
+        cross.zero(S.stream);
         hipLaunchKernelGGL(k_block_normal_tab, dim3(grid_for(S.nblk * npk)), dim3(BLOCK), 0, S.stream, S.nblk,
                            S.blk_kmax, S.blk_ptr.p, S.blk_cols.p, S.blk_full.p, S.GdT.rp.p, S.GdT.ci.p, S.GdT.val.p,
-                           S.rs.p, bd, S.blk_tab.p, S.blk_Ri.p);
+                           S.rs.p, bd, S.blk_tab.p, S.blk_Ri.p, cross.p);
+        KERNEL_CHECK();
+        int c = 0;
+        cross.download(&c, 1, S.stream);
+        HIP_CHECK(hipStreamSynchronize(S.stream));
+        tab_done = c == 0;
+    }
+    if (tab_done) {
     } else if (!S.g_full)   // lazily formed structured system: GdT + the stencil parts
         hipLaunchKernelGGL(k_block_normal_mf, dim3(grid_for(S.nblk * npk)), dim3(BLOCK), 0, S.stream, S.nblk,
                            S.blk_kmax, S.blk_ptr.p, S.blk_cols.p, S.blk_full.p, S.GdT.rp.p, S.GdT.ci.p, S.GdT.val.p,

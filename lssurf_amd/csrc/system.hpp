@@ -285,6 +285,7 @@ struct CgState {
     // other ping-pong buffer); pend = 1 while α_k p_k is owed (pend_buf: which buffer holds p_k)
     int32_t pend, pend_buf;
     double pend_alpha;
+    double anorm_seed;   // lsq_opts.anorm0: the stopping rule's ‖A‖ is max(seed, sqrt(anorm2))
 };
 
 struct System {
@@ -356,8 +357,8 @@ struct System {
     DBuf<int32_t> blk_cols;         // compact ids
     DBuf<int32_t> blk_full;         // full ids (stencil operator v-space)
     DBuf<double> blk_Ri;
-    DBuf<double> blk_tab;
-    bool dist_graph_failed = false;   // a rank's batch capture was refused once: eager from then on           // lazily formed systems: the block-diagonal stencil class tables (block.hip)
+    DBuf<double> blk_tab;           // lazily formed systems: the block-diagonal stencil class tables (block.hip)
+    bool dist_graph_failed = false; // a rank's batch capture was refused once: eager from then on
     DBuf<lf_t> blk_Lf;              // R_b⁻¹ as CGNR streams it (lf_t, packed upper, block stride lf_stride(npk))
     DBuf<double> blk_tmp;           // structured ranks: block partial sums by column (kmax × n_full) for the halo
     bool blk_valid = false;
@@ -516,12 +517,13 @@ void describe_global(System& S, int64_t n_full, int32_t n_grids, const lsq_grid_
                      const lsq_stencil_desc* st);   // S.dg_mfh (lsq_dist_set_global)
 void build_dmf(System& S, int32_t n_grids, const lsq_grid_desc* grids, int32_t n_interp, const int32_t* interp_grid,
                int64_t npts, const double* py, const double* px, const double* pt);   // S.dmf (CGNR data rows)
+void shape_counts(System& S, int64_t* mk, int64_t* zk);   // assemble.hip: kept rows / entries (lsq_shape)
 void ensure_sell(System& S);                    // assembled A / AT (lazy when S.mf)
 void refresh_scaling(System& S, int precond);
 // band.hip: sqrt(diag((AᵀA)⁻¹)) and op-row variances from a banded Cholesky + Takahashi inverse
 void band_factor(System& S, const int32_t* perm, BandFactor& F, int64_t nw = -1);   // nw ≥ 0: a column window
-void graph_cache_drop(const System* S);
-void upload_row_mask(System& S, const uint8_t* keep);   // build.hip: rowkeep ← keep (non-zero → 1)   // lsqr.hip: captured iteration batches of S
+void graph_cache_drop(const System* S);   // lsqr.hip: captured iteration batches of S
+void upload_row_mask(System& S, const uint8_t* keep);   // build.hip: rowkeep ← keep (non-zero → 1)
 void band_solve_scratch(System& S);
 void band_precond(System& S);   // S.band from S.band_order (precond 5)
 void band_launch_bsub(System& S, const double* v, int scale_mode, double* out);

@@ -496,6 +496,14 @@ class DistFitSystem(_Base):
         self.L.lsq_sell_info(self.h, ptr(o))
         return dict(zip(['m', 'n', 'nnz', 'sell_A', 'sell_AT', 'device_bytes', 'stencil_op', 'n_full'], o.tolist()))
 
+    def comm_info(self):
+        """What this rank's RCCL communicator and device report (lsq_dist_comm_info): comm_count,
+        comm_rank, comm_device, device and the card's PCI id (domain:bus:device)."""
+        o = np.zeros(7, np.int64)
+        _HandleView(self.L, self.h).check(self.L.lsq_dist_comm_info(self.h, ptr(o)), 'lsq_dist_comm_info')
+        return {'comm_count': int(o[0]), 'comm_rank': int(o[1]), 'comm_device': int(o[2]), 'device': int(o[3]),
+                'pci': f'{int(o[4]):04x}:{int(o[5]):02x}:{int(o[6]):02x}'}
+
     def close(self):
         if getattr(self, 'h', None):
             self.L.lsq_destroy(self.h)
@@ -633,9 +641,11 @@ class VirtualDistFitSystem(_Base):
             out[prob['l2g']] += loc
         return out
 
-    def solve(self, row_weight, rhs, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, method=0, x0=None):
+    def solve(self, row_weight, rhs, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, method=0, x0=None,
+              anorm0=0.0):
         """x0 (global compact, CGNR on structured ranks): warm start; each rank starts from x0 on
-        its window's columns."""
+        its window's columns.  anorm0 (CGNR): the stopping rule's starting ‖A‖ estimate
+        (lsq_opts.anorm0; every rank runs the same scalar recurrence, so one value for all)."""
         bs = self._bs(row_weight, rhs)
         warm = x0 is not None and self.structured and int(method) == 1
         if warm:
@@ -645,7 +655,7 @@ class VirtualDistFitSystem(_Base):
         bp = (ctypes.c_void_p * self.nranks)(*[b.ctypes.data for b in bs])
         xp = (ctypes.c_void_p * self.nranks)(*[x.ctypes.data for x in xs])
         o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond), method=int(method),
-                         use_x0=int(warm))
+                         use_x0=int(warm), anorm0=float(anorm0))
         st = LsqStats()
         self._check(self._fn('solve')(self.g, bp, xp, ctypes.byref(o), ctypes.byref(st)), f'{self._api}_solve')
         self.stats = st.as_dict()
@@ -718,7 +728,8 @@ class MultiDeviceFitSystem:
         else:
             self._rhs_last = rhs
         x = self.group.solve(None, rhs, x0=x0, **{k: v for k, v in opts.items()
-                                                   if k in ('atol', 'btol', 'conlim', 'maxit', 'precond', 'method')})
+                                                   if k in ('atol', 'btol', 'conlim', 'maxit', 'precond', 'method',
+                                                            'anorm0')})
         self.stats = self.group.stats
         return x
 

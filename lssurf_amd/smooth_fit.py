@@ -51,7 +51,7 @@ DEFAULTS = {'reference_epoch': 0, 'W_ctr': 1e4, 'return_fit_objects': False, 'ma
             # the tolerance documented in DESIGN.md §Parity)
             'device': 0, 'lsq_atol': 1e-12, 'lsq_btol': 1e-12, 'lsq_conlim': 1e12, 'lsq_maxit': 0,
             'lsq_precond': 'auto', 'lsq_dense_max': 16384, 'lsq_warm_start': True, 'lsq_method': 'auto',
-            'lsq_E_method': 'auto', 'n_gpus': 1, 'devices': None}
+            'lsq_reuse_anorm': True, 'lsq_E_method': 'auto', 'n_gpus': 1, 'devices': None}
 
 OUT_OF_SCOPE = ('bias_params', 'sensor_grid_bias_params', 'prior_args', 'prior_edge_args', 'lagrangian_coords',
                 'constraint_scaling_maps', 'mask_file', 'bias_edit_vals')
@@ -202,8 +202,12 @@ def iterate_fit(data, system, rhs, TCinv, G_data, Gc, in_TSE, timing, args, grid
     rs_data = None
     timing['lsq_iters'] = 0
     # row weights 1/sqrt(E_all²) with E_all = 1/TCinv (smooth_fit.py:103, 129): |TCinv| — the caller's
-    # array itself when positive (no pass over, or copy of, the 77 M rows at C4)
-    weight0 = TCinv if TCinv.min() > 0 else np.abs(TCinv)
+    # array itself when positive (no pass over, or copy of, the 77 M rows at C4).  sqrt(fl(x²)) = |x|
+    # in IEEE arithmetic, so the reference's weight is 1/|fl(1/TCinv)|, which can differ from |TCinv|
+    # by one ulp (a relative 1e-16 change of a row weight; DESIGN.md §4 records the deviation).  The
+    # weights are a read-only view: nothing may edit them in place, since they alias TCinv.
+    weight0 = (TCinv if TCinv.min() > 0 else np.abs(TCinv)).view()
+    weight0.flags.writeable = False
     for iteration in range(args['max_iterations']):
         weight = weight0
         if last_iteration and args['sigma_extra_relax']:
@@ -223,6 +227,13 @@ def iterate_fit(data, system, rhs, TCinv, G_data, Gc, in_TSE, timing, args, grid
         if mg and 'mg_build' not in timing:
             timing['mg_build'] = system.mg_build_s
         opts = _solve_opts(args, system.keep_cols.size, system.has_blocks, mg, dense_ok)
+        last = system.stats
+        if args['lsq_reuse_anorm'] and last is not None and last.get('method') == 1 and \
+                opts['method'] == 1 and last.get('precond') == opts['precond']:
+            # the CGNR stopping rule starts from the previous solve's ‖A M^-1/2‖ estimate (lsq_opts
+            # .anorm0) instead of rebuilding it from zero: with node-block M the preconditioned
+            # Frobenius norm is sqrt(n) whatever the weights, so the estimate stays below it
+            opts['anorm0'] = float(last['anorm'])
         try:
             x = system.solve(weight, in_TSE, rhs, x0=x0, **opts)
         except NativeError as e:
@@ -233,11 +244,12 @@ def iterate_fit(data, system, rhs, TCinv, G_data, Gc, in_TSE, timing, args, grid
             print(f'smooth_fit: multigrid preconditioner unavailable ({e}); block-Jacobi for the rest of '
                   f'the fit', flush=True)
             system._mg = False
-            x = system.solve(weight, in_TSE, rhs, x0=x0,
-                             **_solve_opts(args, system.keep_cols.size, system.has_blocks, False, dense_ok))
+            opts = _solve_opts(args, system.keep_cols.size, system.has_blocks, False, dense_ok)
+            x = system.solve(weight, in_TSE, rhs, x0=x0, **opts)
         if system.stats['istop'] == 7:
             print(f"smooth_fit: LSQR reached its iteration limit ({system.stats['iters']}) before the "
                   f"requested tolerance; raise lsq_maxit or use lsq_precond=2", flush=True)
+        system.stats['precond'] = opts['precond']
         m0 = system.expand(x)
         timing['sparseqr_solve'] = time() - tic
         timing['lsq_iters'] += int(system.stats['iters'])

@@ -143,21 +143,23 @@ class LSQSolver:
 
     # ---- solve -------------------------------------------------------------------------------
     def solve(self, b, x0=None, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, batch=0,
-              use_graph=True, op=0, method=0, b_rows=0):
+              use_graph=True, op=0, method=0, b_rows=0, anorm0=0.0):
         """LSQR (method 0) or CGNR (method 1: PCG on the normal equations with the fused
         normal-stencil operator; LSQR where that operator does not exist — stats['method'] says
         which ran); returns (x, stats) with scipy-lsqr-style stats (iters, istop, r1norm, ...).
         precond: 1 Jacobi, 2 dense Cholesky, 3 block-Jacobi per node, 4 multigrid V-cycle (CGNR
         only).  batch 0: the library's default iterations per host convergence check.  b_rows > 0:
         the caller guarantees b[b_rows:] == 0, so only b[:b_rows] crosses PCIe (smooth_fit: the
-        data rows; the 73 M constraint rows of C4 are zero)."""
+        data rows; the 73 M constraint rows of C4 are zero).  anorm0 (CGNR): stats['anorm'] of an
+        earlier solve of the same operator and preconditioner — the stopping rule starts from it
+        instead of rebuilding its ‖A‖ estimate (lsq_opts.anorm0)."""
         b = as_c(b, np.float64)
         if b.size != self.m:
             raise ValueError(f'b has {b.size} rows, system has {self.m}')
         x = np.zeros(self.n) if x0 is None else as_c(x0, np.float64).copy()
         o = default_opts(atol=atol, btol=btol, conlim=conlim, maxit=int(maxit), precond=int(precond),
                          use_x0=int(x0 is not None), batch=int(batch), use_graph=int(bool(use_graph)), op=int(op),
-                         method=int(method), b_rows=int(b_rows))
+                         method=int(method), b_rows=int(b_rows), anorm0=float(anorm0))
         st = LsqStats()
         self._check(self._L.lsq_solve(self._h, ptr(b), ptr(x), ctypes.byref(o), ctypes.byref(st)), 'lsq_solve')
         return x, st.as_dict()

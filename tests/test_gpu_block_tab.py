@@ -57,3 +57,36 @@ def test_block_normal_table_matches_descriptor_kernel(gpu_available, which):
     xb, sb = _run(which, '1', 0)
     assert abs(sa['iters'] - sb['iters']) <= 2
     assert np.linalg.norm(xb - xa) / np.linalg.norm(xa) <= 1e-8
+
+
+def test_block_spanning_nodes_takes_descriptor_kernel(gpu_available):
+    """A user block that pairs two (y, x) nodes of one grid (here the z0 columns of x-neighbours,
+    coupled by the z0 curvature stencil): the class tables hold only the stencil terms inside one
+    node, so the table kernel flags the block and the normals come from the part descriptors —
+    the same iterates as LSQ_BLK_TAB=0 (without the flag they silently differed)."""
+    def run(tab):
+        saved = os.environ.get('LSQ_BLK_TAB')
+        os.environ['LSQ_BLK_TAB'] = tab
+        try:
+            S, fs, w, rhs = _synthetic_system('t64')
+            try:
+                z0 = np.asarray(S['G_data'].TOC['cols']['z0']).ravel()
+                ny, nx = S['grids']['z0'].shape
+                pos = np.searchsorted(fs.keep_cols, z0).reshape(ny, nx)
+                blocks = [np.array([pos[y, 2 * i], pos[y, 2 * i + 1]]) for y in range(ny) for i in range(nx // 2)]
+                fs.solver.set_column_blocks(blocks)
+                fs.solver.set_row_weight(w)
+                fs.solver.set_row_mask(np.ones(w.size, bool))
+                return fs.solver.solve(rhs, atol=1e-12, btol=1e-12, conlim=1e12, maxit=30, precond=3, method=1)
+            finally:
+                fs.close()
+        finally:
+            if saved is None:
+                os.environ.pop('LSQ_BLK_TAB', None)
+            else:
+                os.environ['LSQ_BLK_TAB'] = saved
+
+    xa, sa = run('0')
+    xb, sb = run('1')
+    assert sa['method'] == sb['method'] == 1
+    assert np.linalg.norm(xb - xa) / np.linalg.norm(xa) <= 1e-10
