@@ -133,8 +133,9 @@ def test_multi_device_warm_start(gpu_available):
 
 def test_single_gpu_resolve_from_solution_with_anorm0(gpu_available):
     """One GPU, multigrid and block-Jacobi CGNR: a re-solve started at x* with the first solve's ‖A‖
-    estimate stops within 5 iterations at x*; without anorm0 it iterates until the estimate rebuilds
-    (scipy's rule, kept as the default of lsq_solve)."""
+    estimate stops within 5 iterations at x*; without anorm0 (scipy's rule, lsq_solve's default) the
+    block-Jacobi re-solve iterates until the estimate rebuilds (the multigrid one: 3 iterations of 44
+    on the first box, its estimate grows fast)."""
     from lssurf_amd.smooth_fit import FitSystem
     S, kw = _t64()
     keep, w, rhs = _problem(S, kw)
@@ -148,7 +149,9 @@ def test_single_gpu_resolve_from_solution_with_anorm0(gpu_available):
             st2 = dict(fs.stats)
             x3 = fs.solve(w, np.ones(fs.n_data, bool), rhs, x0=x1, **opts)
             st3 = dict(fs.stats)
-            assert st2['iters'] <= 5 < st3['iters'], (precond, st1['iters'], st2['iters'], st3['iters'])
+            assert st2['iters'] <= min(5, st3['iters']), (precond, st1['iters'], st2['iters'], st3['iters'])
+            if precond == 3:   # block-Jacobi: the unseeded rule rebuilds its estimate (measured 48 of 523 on
+                assert st3['iters'] > 5, (st1['iters'], st3['iters'])   # two ranks); multigrid: 3 of 44
             assert st2['anorm'] >= st1['anorm']
             assert np.linalg.norm(x2 - x1) <= 1e-9 * np.linalg.norm(x1)
             assert np.linalg.norm(x3 - x1) <= 1e-7 * np.linalg.norm(x1)
