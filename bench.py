@@ -136,20 +136,41 @@ class _Dist:
         return d
 
 
-def cpu_baseline(fs, b_weighted, sample_iters, threads, method=0):
-    """The same algorithm on this host's cores, on the same formed A (downloaded from the device)
-    and the same weighted rhs, a bounded sample of iterations: CGNR + block-Jacobi with the GPU
-    solve's node blocks (oracle/cgnr_cpu.c) when the GPU line is CGNR, else LSQR
-    (oracle/lsqr_cpu.c)."""
+def cpu_baseline(fs, w, b_weighted, sample_iters, threads, method=0):
+    """The same algorithm on this host's cores, on the same system and the same weighted rhs, a
+    bounded sample of iterations: CGNR + block-Jacobi with the GPU solve's node blocks when the GPU
+    line is CGNR — on the GPU's operator representation (oracle/cgnr_struct_cpu.c: stencil rows from
+    the part descriptors, matrix-free data rows; `value`) and on the assembled CSR downloaded from the
+    device (oracle/cgnr_cpu.c; `csr_port`) — else LSQR (oracle/lsqr_cpu.c)."""
     from oracle import cpu
-    A = fs.solver.get_csr()
     if method == 1 and getattr(fs, 'blocks', None) is not None:
+        out = None
+        if getattr(fs, 'desc', None) is not None:
+            try:
+                # half the CSR kind's sample: ~0.35 s per C4 iteration on 16 threads (two passes over
+                # the 75 M rows and their weights, no stored matrix) against the CSR kind's ~0.14 s
+                xs, st = cpu.cgnr_bj_struct(fs.desc, fs.n_full, w, fs.keep_cols, b_weighted, *fs.blocks,
+                                            fixed_iters=max(10, sample_iters // 2), threads=threads)
+                out = {'value': st['iters'] / st['time_s'], 'unit': 'CGNR iters/s', 'cores': int(st['threads']),
+                       'kind': 'port', 'setup_s': st['setup_s'], 'operator': 'structured (matrix-free)',
+                       'sample': f'{int(st["iters"])} CGNR + block-Jacobi iterations of the same system and node '
+                                 f'blocks on the GPU line\'s operator representation (stencil rows from the part '
+                                 f'descriptors, matrix-free data rows; oracle/cgnr_struct_cpu.c, OpenMP), '
+                                 f'{st["time_s"]:.1f} s after {st["setup_s"]:.1f} s of point sort and block factors'}
+            except ValueError as e:   # interpolation grids on different lattices: the CSR kind only
+                log(f'bench: structured CPU baseline unavailable ({e})')
+        A = fs.solver.get_csr()
         x, st = cpu.cgnr_bj(A, b_weighted, *fs.blocks, fixed_iters=sample_iters, threads=threads)
-        return {'value': st['iters'] / st['time_s'], 'unit': 'CGNR iters/s', 'cores': int(st['threads']),
-                'kind': 'port', 'setup_s': st['setup_s'],
-                'sample': f'{int(st["iters"])} CGNR + block-Jacobi iterations of the same system and node blocks '
-                          f'(oracle/cgnr_cpu.c, OpenMP; the GPU line\'s algorithm), {st["time_s"]:.1f} s '
-                          f'after {st["setup_s"]:.1f} s of transpose and block factors'}
+        csr = {'value': st['iters'] / st['time_s'], 'unit': 'CGNR iters/s', 'cores': int(st['threads']),
+               'kind': 'port', 'setup_s': st['setup_s'], 'operator': 'assembled CSR',
+               'sample': f'{int(st["iters"])} CGNR + block-Jacobi iterations of the same system and node blocks '
+                         f'on the assembled CSR (oracle/cgnr_cpu.c, OpenMP), {st["time_s"]:.1f} s after '
+                         f'{st["setup_s"]:.1f} s of transpose and block factors'}
+        if out is None:
+            return csr
+        out['csr_port'] = csr
+        return out
+    A = fs.solver.get_csr()
     x, st = cpu.lsqr(A, b_weighted, fixed_iters=sample_iters, threads=threads)
     return {'value': st['iters'] / st['time_s'], 'unit': 'LSQR iters/s', 'cores': int(st['threads']),
             'kind': 'port', 'sample': f'{int(st["iters"])} LSQR iterations of the same system (oracle/lsqr_cpu.c, '
@@ -420,7 +441,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not args.dist:
         threads = min(os.cpu_count() or 1, 16)
-        cpu = cpu_baseline(fs, w * rhs, args.cpu_iters, threads, meth)
+        cpu = cpu_baseline(fs, w, w * rhs, args.cpu_iters, threads, meth)
         if args.cpu_solve and solve:   # the CPU oracle to the same stopping rule, on the same A, b
             from oracle import cpu as ocpu
             xc, stc = ocpu.lsqr(fs.solver.get_csr(), w * rhs, atol=1e-10, btol=1e-10, conlim=1e8,

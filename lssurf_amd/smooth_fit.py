@@ -69,6 +69,7 @@ class FitSystem:
         self.solver.set_col_map(self.n_full, keep_cols)
         m = self.n_data + self.n_con
         desc = describe(G_data, Gc, with_fields=True) if structured else None
+        self.desc = desc           # the descriptors (bench.py's structured CPU baseline reads them)
         self.formation = 'stencil' if desc is not None else 'coo'
         if desc is not None:       # rows generated on the device from the grids and stencils
             gdesc, interp, coords, stencils, npts, fields = desc

@@ -1,6 +1,7 @@
 """ctypes wrappers for the oracle's C restatements (TEST INFRASTRUCTURE ONLY).
 
-build() compiles oracle/lsqr_cpu.c + oracle/cgnr_cpu.c + oracle/tri_upper.c into oracle/_cpu.so with gcc -O2
+build() compiles oracle/lsqr_cpu.c + oracle/cgnr_cpu.c + oracle/cgnr_struct_cpu.c + oracle/tri_upper.c into
+oracle/_cpu.so with gcc -O2
 -fopenmp (no -march: plain SSE2 doubles, no FMA — matching the reference's Cython build).
 """
 import ctypes
@@ -12,7 +13,8 @@ import scipy.sparse as sp
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, '_cpu.so')
-SRC = [os.path.join(HERE, 'lsqr_cpu.c'), os.path.join(HERE, 'cgnr_cpu.c'), os.path.join(HERE, 'tri_upper.c')]
+SRC = [os.path.join(HERE, 'lsqr_cpu.c'), os.path.join(HERE, 'cgnr_cpu.c'), os.path.join(HERE, 'cgnr_struct_cpu.c'),
+       os.path.join(HERE, 'tri_upper.c')]
 _lib = None
 
 
@@ -35,6 +37,9 @@ def lib():
         L.lsqr_cpu.restype = ctypes.c_int
         L.cgnr_bj_cpu.argtypes = [i64, i64, P, P, P, P, i64, P, P, P, f64, i64, i64, ctypes.c_int, P]
         L.cgnr_bj_cpu.restype = ctypes.c_int
+        L.cgnr_bj_struct_cpu.argtypes = [i32, P, i32, P, i64, P, P, P, i32, P, i64, i64, P, i64, P, P, i64, P, P, P,
+                                         f64, i64, i64, ctypes.c_int, P]
+        L.cgnr_bj_struct_cpu.restype = ctypes.c_int
         L.oracle_inv_tr_upper.argtypes = [i64, P, P, P, i64, f32, P, P, P, P]
         L.oracle_inv_tr_upper.restype = ctypes.c_int
         L.oracle_propagate_qz_errors.argtypes = [i64, P, P, P, P]
@@ -80,6 +85,41 @@ def cgnr_bj(A, b, block_ptr, block_cols, atol=1e-10, maxit=0, fixed_iters=0, thr
                            fixed_iters, threads, _p(st))
     if rc != 0:
         raise ValueError('cgnr_bj: a block has more than 16 columns')
+    keys = ['iters', 'time_s', 'setup_s', 'threads', 'snorm', 'rnorm', 'anorm_f']
+    return x, dict(zip(keys, st.tolist()))
+
+
+def cgnr_bj_struct(desc, n_full, row_scale, keep_cols, b, block_ptr, block_cols, atol=1e-10, maxit=0,
+                   fixed_iters=0, threads=0):
+    """CPU CGNR + block-Jacobi on the STRUCTURED operator (oracle/cgnr_struct_cpu.c: stencil rows from
+    the part descriptors, matrix-free data rows from the sorted points — the GPU line's operator
+    representation, no stored matrix).  desc: lssurf_amd.assemble.describe(G_data, Gc) (grids,
+    interp grid ids, (py, px, pt), stencils, npts); row_scale: row weights × mask (m); keep_cols:
+    compact -> full column ids; b: the weighted rhs (m).  Returns (x, stats) as cgnr_bj; raises
+    ValueError when the interpolation grids do not share one (y, x) lattice."""
+    grids, interp, (py, px, pt), stencils, npts = desc[:5]
+    if len(desc) > 5 and desc[5]:
+        raise ValueError('cgnr_bj_struct: field-valued stencil parts are not supported')
+    ga = (type(grids[0]) * len(grids))(*grids)
+    sa = (type(stencils[0]) * len(stencils))(*stencils)
+    ig = np.ascontiguousarray(interp, dtype=np.int32)
+    rs = np.ascontiguousarray(row_scale, dtype=np.float64)
+    kc = np.ascontiguousarray(keep_cols, dtype=np.int64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    bp = np.ascontiguousarray(block_ptr, dtype=np.int64)
+    bc = np.ascontiguousarray(block_cols, dtype=np.int32)
+    py, px = np.ascontiguousarray(py, np.float64), np.ascontiguousarray(px, np.float64)
+    ptv = None if pt is None else np.ascontiguousarray(pt, np.float64)
+    x = np.zeros(kc.size)
+    st = np.zeros(7)
+    rc = lib().cgnr_bj_struct_cpu(len(grids), ctypes.cast(ga, ctypes.c_void_p), ig.size, _p(ig), int(npts), _p(py),
+                                  _p(px), None if ptv is None else _p(ptv), len(stencils),
+                                  ctypes.cast(sa, ctypes.c_void_p), rs.size, int(n_full), _p(rs), kc.size, _p(kc),
+                                  _p(b), bp.size - 1, _p(bp), _p(bc), _p(x), atol, maxit, fixed_iters, threads, _p(st))
+    if rc == -2:
+        raise ValueError('cgnr_bj_struct: the interpolation grids do not share one (y, x) lattice')
+    if rc != 0:
+        raise ValueError('cgnr_bj_struct: a block has more than 16 columns')
     keys = ['iters', 'time_s', 'setup_s', 'threads', 'snorm', 'rnorm', 'anorm_f']
     return x, dict(zip(keys, st.tolist()))
 
