@@ -51,6 +51,43 @@ def test_mg_level_operators_match_host_galerkin(gpu_available, which):
         fs.close()
 
 
+@pytest.mark.parametrize('kt', ['0', '1', '2'])
+def test_mg_tile_kernels_match_host_galerkin(gpu_available, kt):
+    """t256: levels 1 and 2 (129² and 65² nodes × 13 columns) run the coarse tile kernel — k_mg_tile
+    (LSQ_MG_TILE_KT=0), or the class-compressed k_mg_tile_kt with scalar (1) or LDS-staged (2, the
+    default) coefficients; every variant's level operator equals the host Galerkin product."""
+    import os
+    saved = os.environ.get('LSQ_MG_TILE_KT')
+    os.environ['LSQ_MG_TILE_KT'] = kt
+    S, fs, w, rhs = _synthetic_system('t256')
+    rng = np.random.default_rng(12)
+    keep = rng.random(fs.n_data) > 0.15
+    try:
+        _prepare(fs, w, keep)
+        levels, tref = fs.solver.mg_info()
+        A = fs.solver.get_csr()
+        ny, nx, nt = S['grids']['dz'].shape
+        host = hierarchy(A, int(keep.sum()), fs.keep_cols, ny, nx, nt)
+        assert len(host) == len(levels), (len(host), levels)
+        for l in (1, 2):
+            (shape, kmask, N), (S0, S1, nf) = host[l], levels[l]
+            assert shape == (S0, S1)
+            if l == 1:
+                assert nf > 1 << 16   # tiled (MG_TILE_MIN)
+            x = np.where(kmask, rng.standard_normal(nf), 0.0)
+            y = fs.solver.mg_apply(l, 0, x)
+            yr = N @ x
+            err = np.abs(y - yr).max() / np.abs(yr).max()
+            assert err <= 1e-11, (l, err)
+            assert np.all(y[~kmask] == 0.0)
+    finally:
+        fs.close()
+        if saved is None:
+            os.environ.pop('LSQ_MG_TILE_KT', None)
+        else:
+            os.environ['LSQ_MG_TILE_KT'] = saved
+
+
 def test_mg_vcycle_is_spd(gpu_available):
     S, fs, w, rhs = _synthetic_system('t64')
     rng = np.random.default_rng(5)
