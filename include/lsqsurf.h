@@ -242,13 +242,16 @@ int lsq_cov_band(lsq_handle* h, const int32_t* perm, double* E, int64_t n_ops, c
 
 /* The same for a WINDOW of the columns (compute_E at scale, lssurf_amd/errors.py method 'window'):
  * perm[0..n_win) lists the window's compact columns in a banded order; the principal submatrix
- * (AᵀA)_WW = A_WᵀA_W (the other columns held fixed) is factored and E[perm[j]] =
- * sqrt(((AᵀA)_WW⁻¹)_jj) for j < n_win (every other E entry 0); op rows must lie inside the window.
- * (AᵀA)⁻¹'s correlations decay with node distance, so the window's interior nodes carry
- * diag((AᵀA)⁻¹) to a tolerance set by the margin (DESIGN.md §Error propagation). */
-int lsq_cov_band_window(lsq_handle* h, const int32_t* perm, int64_t n_win, double* E, int64_t n_ops,
-                        const int64_t* op_ptr, const int32_t* op_col, const double* op_val, double* op_err,
-                        int64_t* info);
+ * (AᵀA)_WW = A_WᵀA_W (the other columns held fixed) is factored and E[j] = sqrt(((AᵀA)_WW⁻¹)_jj)
+ * in WINDOW order (n_win entries).  inner (nullable = every position): only the 64-column tiles
+ * of the window order that hold a flagged position are swept (the interior whose σ the caller
+ * keeps — the margin's sweeps are most of the work), and E is 0 at the other positions.  op rows
+ * must lie inside the window.  (AᵀA)⁻¹'s correlations decay with node distance, so the window's
+ * interior nodes carry diag((AᵀA)⁻¹) to a tolerance set by the margin (DESIGN.md §Error
+ * propagation). */
+int lsq_cov_band_window(lsq_handle* h, const int32_t* perm, int64_t n_win, const uint8_t* inner, double* E,
+                        int64_t n_ops, const int64_t* op_ptr, const int32_t* op_col, const double* op_val,
+                        double* op_err, int64_t* info);
 
 /* The banded factor itself (replaces sparseqr.rz's R and E, smooth_fit.py:218 / the aniso notebook):
  * for the current weighted, masked A and the column order perm (nullable = natural),

@@ -105,7 +105,7 @@ def load():
         'lsq_sigma_x': ([P, P], ctypes.c_int),
         'lsq_get_rinv': ([P, P], ctypes.c_int),
         'lsq_cov_band': ([P, P, P, ctypes.c_int64, P, P, P, P, P], ctypes.c_int),
-        'lsq_cov_band_window': ([P, P, i64, P, i64, P, P, P, P, P], ctypes.c_int),
+        'lsq_cov_band_window': ([P, P, i64, P, P, i64, P, P, P, P, P], ctypes.c_int),
         'lsq_set_band_order': ([P, ctypes.c_int64, P], ctypes.c_int),
         'lsq_band_factor': ([P, P, P, P, P, P], ctypes.c_int),
         'lsq_dist_unique_id': ([P], ctypes.c_int),

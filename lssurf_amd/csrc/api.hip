@@ -620,16 +620,16 @@ int lsq_cov_band(lsq_handle* h, const int32_t* perm, double* E, int64_t n_ops, c
     });
 }
 
-int lsq_cov_band_window(lsq_handle* h, const int32_t* perm, int64_t n_win, double* E, int64_t n_ops,
-                        const int64_t* op_ptr, const int32_t* op_col, const double* op_val, double* op_err,
-                        int64_t* info) {
+int lsq_cov_band_window(lsq_handle* h, const int32_t* perm, int64_t n_win, const uint8_t* inner, double* E,
+                        int64_t n_ops, const int64_t* op_ptr, const int32_t* op_col, const double* op_val,
+                        double* op_err, int64_t* info) {
     return guarded(h, [&](lsq::System& S) {
         if (!S.G.rp.p) return fail(S, "lsq_cov_band_window: no matrix");
         if (S.dist) return fail(S, "lsq_cov_band_window: not available on distributed handles");
         if (!E || !perm || n_win < 1 || n_win > S.G.n) return fail(S, "lsq_cov_band_window: bad window");
         if (n_ops < 0 || (n_ops > 0 && (!op_ptr || !op_err || (op_ptr[n_ops] > 0 && (!op_col || !op_val)))))
             return fail(S, "lsq_cov_band_window: bad op rows");
-        lsq::band_cov(S, perm, n_win, E, n_ops, op_ptr, op_col, op_val, op_err, info);
+        lsq::band_cov(S, perm, n_win, E, n_ops, op_ptr, op_col, op_val, op_err, info, inner);
         return 0;
     });
 }

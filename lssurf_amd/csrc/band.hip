@@ -384,7 +384,8 @@ __global__ __launch_bounds__(BLOCK) void k_band_syrk(BandDev b, int64_t K, int m
 // non-zero row K0: Y_K = D_Kᵀ (O_K − Σ_{I=max(K0,K−w)}^{K−1} R_IKᵀ Y_I); out = ‖y‖² per right-hand
 // side.  Only the last w+1 tiles of y are live: a ring per workgroup (the __threadfence closing
 // each step also invalidates this CU's L1, so a rewritten slot is read fresh).
-// IDENT: o = e_{64J..64J+63}, J = j0 + blockIdx.x (the diagonal of N⁻¹).  Otherwise op rows: the
+// IDENT: o = e_{64J..64J+63}, J = j0 + blockIdx.x, or J = sp[blockIdx.x] when sp is given (the
+// tiles of a window's interior), out at tile J (the diagonal of N⁻¹).  Otherwise op rows: the
 // workgroup's segments [sp[rt], sp[rt+1]) each hold one tile row segK[s] and the entries
 // [segE[s], segE[s+1]) as (row-in-tile << 6 | rhs) in el and the value in ev (× s_j here).
 template <bool IDENT>
@@ -401,7 +402,7 @@ __global__ __launch_bounds__(BLOCK) void k_band_sweep(BandDev b, int64_t j0, con
     double* Rg = ring + rt * W1 * TT;
     int64_t s = 0, s1 = 0, K0 = 0;
     if (IDENT) {
-        K0 = j0 + rt;
+        K0 = sp ? sp[rt] : j0 + rt;
     } else {
         s = sp[rt];
         s1 = sp[rt + 1];
@@ -461,16 +462,16 @@ __global__ __launch_bounds__(BLOCK) void k_band_sweep(BandDev b, int64_t j0, con
         double sum = 0.0;
         for (int wr = 0; wr < 2; ++wr)
             for (int lk = 0; lk < 4; ++lk) sum += red[wr * 2 + half][lk][t][li];
-        out[((IDENT ? j0 : 0) + rt) * TB + c] = sum;
+        out[(IDENT ? K0 : rt) * TB + c] = sum;
     }
 }
 
-// E[perm[j]] = sqrt(ss_j)·s_j from the identity sweeps
+// E[perm[j]] = sqrt(ss_j)·s_j from the identity sweeps (perm null: E[j], window order)
 __global__ __launch_bounds__(BLOCK) void k_band_diag_sweep(int64_t n, const int32_t* __restrict__ perm,
                                                            const double* __restrict__ ssq,
                                                            const double* __restrict__ sc, double* __restrict__ E) {
     for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLOCK)
-        E[perm[j]] = sqrt(ssq[j]) * sc[j];
+        E[perm ? perm[j] : j] = sqrt(ssq[j]) * sc[j];
 }
 
 // ---- precond 5: LSQR on A·M, M = P·S·R̃⁻¹ (lsqr.hip) ------------------------------------------
@@ -746,9 +747,9 @@ void run_sweeps(hipStream_t st, const BandDev& b, int64_t nwg, int64_t cap, cons
                 const int64_t* segE, const int32_t* el, const double* ev, const double* sc, double* ring, double* out) {
     for (int64_t g0 = 0; g0 < nwg; g0 += cap) {
         const int64_t g = std::min(cap, nwg - g0);
-        if (IDENT)
-            hipLaunchKernelGGL(k_band_sweep<true>, dim3((unsigned)g), dim3(BLOCK), 0, st, b, g0, sp, segK, segE, el, ev,
-                               sc, ring, out);
+        if (IDENT)   // sp: the tiles to sweep (null: tiles g0 … g0 + g − 1)
+            hipLaunchKernelGGL(k_band_sweep<true>, dim3((unsigned)g), dim3(BLOCK), 0, st, b, g0, sp ? sp + g0 : nullptr,
+                               segK, segE, el, ev, sc, ring, out);
         else
             hipLaunchKernelGGL(k_band_sweep<false>, dim3((unsigned)g), dim3(BLOCK), 0, st, b, (int64_t)0, sp + g0, segK,
                                segE, el, ev, sc, ring, out + g0 * TB);
@@ -944,7 +945,7 @@ void band_factor_download(System& S, const int32_t* h_perm, int64_t* info, doubl
 }
 
 void band_cov(System& S, const int32_t* h_perm, int64_t nw, double* h_E, int64_t nops, const int64_t* h_rp,
-              const int32_t* h_ci, const double* h_v, double* h_oe, int64_t* info) {
+              const int32_t* h_ci, const double* h_v, double* h_oe, int64_t* info, const uint8_t* inner) {
     hipStream_t st = S.stream;
     refresh_scaling(S, S.cs_mode < 0 ? 0 : S.cs_mode);
     const int64_t ncol = S.G.n;
@@ -978,16 +979,39 @@ void band_cov(System& S, const int32_t* h_perm, int64_t nw, double* h_E, int64_t
     const int64_t nop_wg = (nops + TB - 1) / TB;
     const int64_t cap = std::min<int64_t>({(int64_t)(0.5 * avail / ring_wg), std::max(T, nop_wg), 1 << 16});
     DBuf<double> ring(cap * (w + 1) * TT);
-    // the diagonal: identity right-hand sides, tile J from row J on
-    DBuf<double> ssq(npad), dE(ncol);
-    if (n < ncol) dE.zero(st);   // a window: the other columns 0
-    run_sweeps<true>(st, b, T, cap, nullptr, nullptr, nullptr, nullptr, nullptr, F.sc.p, ring.p, ssq.p);
-    hipLaunchKernelGGL(k_band_diag_sweep, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, F.perm.p, ssq.p, F.sc.p, dE.p);
+    // the diagonal: identity right-hand sides, tile J from row J on — every tile, or (a window's
+    // interior) the tiles holding an inner position: their sweeps are the window's whole result
+    std::vector<int64_t> tiles;
+    if (nw >= 0 && inner) {
+        for (int64_t J = 0; J < T; ++J) {
+            bool any = false;
+            for (int64_t j = J * TB; j < std::min<int64_t>(n, (J + 1) * TB) && !any; ++j) any = inner[j] != 0;
+            if (any) tiles.push_back(J);
+        }
+    } else {
+        tiles.resize(T);
+        for (int64_t J = 0; J < T; ++J) tiles[J] = J;
+    }
+    const int64_t nsw = (int64_t)tiles.size();
+    const int64_t nE = nw >= 0 ? n : ncol;   // a window: E in window order
+    DBuf<double> ssq(npad), dE(std::max<int64_t>(nE, 1));
+    DBuf<int64_t> dtiles(std::max<int64_t>(nsw, 1));
+    ssq.zero(st);   // tiles not swept: E = 0
+    if (nw < 0 && n < ncol) dE.zero(st);
+    if (nsw > 0) {
+        dtiles.upload(tiles.data(), nsw, st);
+        run_sweeps<true>(st, b, nsw, cap, dtiles.p, nullptr, nullptr, nullptr, nullptr, F.sc.p, ring.p, ssq.p);
+    }
+    hipLaunchKernelGGL(k_band_diag_sweep, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, nw >= 0 ? nullptr : F.perm.p,
+                       ssq.p, F.sc.p, dE.p);
     KERNEL_CHECK();
-    dE.download(h_E, ncol, st);
+    dE.download(h_E, nE, st);
     HIP_CHECK(hipStreamSynchronize(st));
+    if (nw >= 0 && inner)
+        for (int64_t j = 0; j < n; ++j)
+            if (!inner[j]) h_E[j] = 0.0;
     int64_t products = 0;
-    for (int64_t J = 0; J < T; ++J) products += (T - J) * (int64_t)std::min<int64_t>(w + 1, T - J);
+    for (int64_t J : tiles) products += (T - J) * (int64_t)std::min<int64_t>(w + 1, T - J);
     if (nops > 0) {
         std::vector<int64_t> rows(nops);
         for (int64_t i = 0; i < nops; ++i) rows[i] = i;

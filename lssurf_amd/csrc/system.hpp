@@ -532,8 +532,10 @@ void band_launch_warm(System& S, const double* x0, double* y0);
 void band_check(System& S);   // throws when a precond-5 solve's grid barrier timed out
 void band_factor_download(System& S, const int32_t* perm, int64_t* info, double* R_out, double* sc_out,
                           int32_t* perm_out);   // sparseqr.rz drop-in (lsq_band_factor)
+// nw ≥ 0 (a window): E in window order (nw entries); inner (nullable): the window positions whose
+// tiles are swept (E 0 elsewhere).  nw < 0: E over every compact column.
 void band_cov(System& S, const int32_t* perm, int64_t nw, double* E, int64_t nops, const int64_t* rp, const int32_t* ci,
-              const double* v, double* op_err, int64_t* info);   // rs/cs -> SELL values (single GPU)
+              const double* v, double* op_err, int64_t* info, const uint8_t* inner = nullptr);   // rs/cs -> SELL values (single GPU)
 void scaling_rows_colnorm(System& S, int precond, bool raw);
 void mf_column_scale(System& S, bool raw);       // lsqr.hip: column norms from the stencil structure
 void scaling_finish_cs(System& S);

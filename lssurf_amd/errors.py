@@ -105,43 +105,65 @@ def window_cov(solver, grids, keep_cols, op=None, tile=WINDOW_TILE, margin=WINDO
         own = (y_lo < oty * tile - margin) | (y_hi >= oty * tile + tile + margin) | \
               (x_lo < otx * tile - margin) | (x_hi >= otx * tile + tile + margin)
 
-    def run(win, inner, rows):
+    # window positions without a pass over all n columns: the band order sorts by node row, so a
+    # window's rows are one contiguous run of it, filtered by node column (round 5: the full-length
+    # masks and the n-long E of every window were ~0.2 s of host work per window at C4)
+    rows_sorted = bool(np.all(iy_o[1:] >= iy_o[:-1]))
+
+    def window(y0, y1, x0, x1):   # band-order positions of the nodes [y0, y1) × [x0, x1)
+        a, b = (np.searchsorted(iy_o, y0, 'left'), np.searchsorted(iy_o, y1, 'left')) if rows_sorted else (0, n)
+        yy, xx = iy_o[a:b], ix_o[a:b]
+        m = (xx >= x0) & (xx < x1)
+        if not rows_sorted:
+            m &= (yy >= y0) & (yy < y1)
+        return a + np.flatnonzero(m)
+
+    def run(pos, inner, rows):
+        """inner: bool per window position (σ kept there, only their tiles swept) or None"""
         sub = op[rows] if rows is not None and rows.size else None
-        Et, oe, info = solver.cov_band_window(order[win], sub)
+        cols = order[pos]
+        Et, oe, info = solver.cov_band_window(cols, sub, inner=inner if inner is not None else np.zeros(pos.size, bool))
         if inner is not None:
-            E[inner] = Et[inner]
+            E[cols[inner]] = Et[inner]
         if sub is not None:
             op_err[rows] = oe
-        return int(info[0])
+        return int(info[0]), int(info[3])
 
     ntiles = nown = 0
-    wmax = 0
+    wmax = products = 0
     for ty in range(0, ny, tile):
         for tx in range(0, nx, tile):
-            win = (iy_o >= ty - margin) & (iy_o < ty + tile + margin) & (ix_o >= tx - margin) & (ix_o < tx + tile + margin)
-            inner = (iy >= ty) & (iy < ty + tile) & (ix >= tx) & (ix < tx + tile)
+            pos = window(ty - margin, ty + tile + margin, tx - margin, tx + tile + margin)
+            yi, xi = iy_o[pos], ix_o[pos]
+            inner = (yi >= ty) & (yi < ty + tile) & (xi >= tx) & (xi < tx + tile)
             rows = None if op is None else np.flatnonzero((oty == ty // tile) & (otx == tx // tile) & ~own)
-            wmax = max(wmax, run(win, inner, rows))
+            w_, p_ = run(pos, inner, rows)
+            wmax, products = max(wmax, w_), products + p_
             ntiles += 1
     if op is not None and own.any():   # one window per distinct support box
         boxes = np.stack([y_lo, y_hi, x_lo, x_hi], axis=1)
         for b in np.unique(boxes[own], axis=0):
             rows = np.flatnonzero(own & np.all(boxes == b, axis=1))
-            win = (iy_o >= b[0] - margin) & (iy_o <= b[1] + margin) & (ix_o >= b[2] - margin) & (ix_o <= b[3] + margin)
-            wmax = max(wmax, run(win, None, rows))
+            pos = window(b[0] - margin, b[1] + margin + 1, b[2] - margin, b[3] + margin + 1)
+            w_, p_ = run(pos, None, rows)
+            wmax, products = max(wmax, w_), products + p_
             nown += 1
     # self-check: the most central tile again with twice the margin; σ of its columns moves by the
     # correlations the margin cut off (conditional vs marginal variance)
     cy, cx = (ny // 2) // tile * tile, (nx // 2) // tile * tile
-    inner = (iy >= cy) & (iy < cy + tile) & (ix >= cx) & (ix < cx + tile)
     m2 = 2 * margin
-    win2 = (iy_o >= cy - m2) & (iy_o < cy + tile + m2) & (ix_o >= cx - m2) & (ix_o < cx + tile + m2)
-    E2, _, _ = solver.cov_band_window(order[win2], None)
-    sel = inner & (E2 > 0)
-    check = float(np.max(np.abs(E[sel] - E2[sel]) / E2[sel])) if sel.any() else 0.0
+    pos2 = window(cy - m2, cy + tile + m2, cx - m2, cx + tile + m2)
+    yi, xi = iy_o[pos2], ix_o[pos2]
+    inner2 = (yi >= cy) & (yi < cy + tile) & (xi >= cx) & (xi < cx + tile)
+    E2, _, _ = solver.cov_band_window(order[pos2], None, inner=inner2)
+    c2 = order[pos2][inner2]
+    e1, e2 = E[c2], E2[inner2]
+    sel = e2 > 0
+    check = float(np.max(np.abs(e1[sel] - e2[sel]) / e2[sel])) if sel.any() else 0.0
     if timing is not None:
         timing['E_window'] = {'tiles': ntiles, 'op_windows': nown, 'tile': tile, 'margin': margin,
-                              'max_band_tiles': wmax, 'selfcheck_rel': check, 'selfcheck_margin': m2}
+                              'max_band_tiles': wmax, 'tile_products': products, 'selfcheck_rel': check,
+                              'selfcheck_margin': m2}
     return E, op_err, check
 
 

@@ -307,23 +307,27 @@ class LSQSolver:
                                          ptr(rp), ptr(ci), ptr(v), ptr(out), ptr(info)), 'lsq_cov_band')
         return E, out, info
 
-    def cov_band_window(self, perm_w, op=None):
+    def cov_band_window(self, perm_w, op=None, inner=None):
         """cov_band for a window W of the columns (perm_w: its compact columns in a banded order):
-        E[c] = sqrt(((A_WᵀA_W)⁻¹)_cc) for c in W (0 elsewhere) and the op rows' errors, every op
-        row inside W (lsq_cov_band_window)."""
-        E = np.zeros(self.n)
-        info = np.zeros(4, np.int64)
+        E[j] = sqrt(((A_WᵀA_W)⁻¹)_jj) in WINDOW order (len(perm_w) entries) and the op rows' errors,
+        every op row inside W (lsq_cov_band_window).  inner (bool per window position, None = all):
+        only the tiles holding those positions are swept; E is 0 elsewhere."""
         pp = as_c(perm_w, np.int32)
+        E = np.zeros(pp.size)
+        info = np.zeros(4, np.int64)
+        ii = None if inner is None else as_c(np.asarray(inner, dtype=bool), np.uint8)
+        if ii is not None and ii.size != pp.size:
+            raise ValueError('cov_band_window: inner must have one flag per window position')
         if op is None or op.shape[0] == 0:
-            self._check(self._L.lsq_cov_band_window(self._h, ptr(pp), pp.size, ptr(E), 0, None, None, None, None,
-                                                    ptr(info)), 'lsq_cov_band_window')
+            self._check(self._L.lsq_cov_band_window(self._h, ptr(pp), pp.size, ptr(ii), ptr(E), 0, None, None, None,
+                                                    None, ptr(info)), 'lsq_cov_band_window')
             return E, np.zeros(0), info
         op = sp.csr_matrix(op)
         op.sort_indices()
         rp, ci, v = as_c(op.indptr, np.int64), as_c(op.indices, np.int32), as_c(op.data, np.float64)
         out = np.zeros(op.shape[0])
-        self._check(self._L.lsq_cov_band_window(self._h, ptr(pp), pp.size, ptr(E), op.shape[0], ptr(rp), ptr(ci),
-                                                ptr(v), ptr(out), ptr(info)), 'lsq_cov_band_window')
+        self._check(self._L.lsq_cov_band_window(self._h, ptr(pp), pp.size, ptr(ii), ptr(E), op.shape[0], ptr(rp),
+                                                ptr(ci), ptr(v), ptr(out), ptr(info)), 'lsq_cov_band_window')
         return E, out, info
 
     def spmv(self, x, trans=False):
