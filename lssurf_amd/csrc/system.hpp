@@ -274,6 +274,14 @@ struct DmfDesc {
 // PCG-on-AᵀA scalar state (device resident).  Quantities are those of CGLS on A·M^{-1/2}; the
 // LSQR estimates (anorm, xnorm of the correction, ‖r‖, ‖Aᵀr‖) follow from the CG scalars through
 // the Lanczos relation.
+// x is updated every CG_XK-th iteration (round 5; every other one before): the step of phase
+// CG_XK − 1 pays x += α_{k−3}p_{k−3} + α_{k−2}p_{k−2} + α_{k−1}p_{k−1} + α_k p_k, the directions of
+// the cycle's phases living in CG_XK buffers (CgP) — the update kernel reads x and four p once per
+// four steps instead of x and two p every other step (4 B per column and step less)
+constexpr int CG_XK = 4;
+struct CgP {   // the direction of the cycle's phase i in p[i]
+    const double* p[CG_XK];
+};
 struct CgState {
     double rho, gamma, alpha, beta, alpha_prev, beta_prev;
     double rn2, bnorm, anorm2, pn2, dp, dn2;
@@ -281,10 +289,8 @@ struct CgState {
     double r1norm, arnorm, xnorm, anorm;
     int64_t itn, maxit;
     int32_t istop, stop, no_stop, pad;
-    // x is updated every other iteration: x += α_{k−1}p_{k−1} + α_k p_k (p_{k−1} is still the
-    // other ping-pong buffer); pend = 1 while α_k p_k is owed (pend_buf: which buffer holds p_k)
-    int32_t pend, pend_buf;
-    double pend_alpha;
+    int32_t pend, pad2;            // steps whose α_k p_k is owed (their phases 0 … pend − 1)
+    double pend_a[CG_XK - 1];      // their α
     double anorm_seed;   // lsq_opts.anorm0: the stopping rule's ‖A‖ is max(seed, sqrt(anorm2))
 };
 
@@ -430,7 +436,8 @@ struct System {
     int32_t mx_z0col = 0, mx_dzcol = 0, mx_Sf0 = 0, mx_Sf1 = 0, mx_Sc0 = 0, mx_Sc1 = 0, mx_nt = 0;
     std::string mg_why;              // why precond 4 is unavailable
     std::vector<double> cg_wkey;   // part row scales the table was built for
-    DBuf<double> cg_x, cg_s, cg_z, cg_p0, cg_p1, cg_q, cg_t, cg_part_g, cg_part_r, cg_part_t;
+    DBuf<double> cg_x, cg_s, cg_z, cg_q, cg_t, cg_part_g, cg_part_r, cg_part_t;
+    DBuf<double> cg_pb[CG_XK];   // the directions of a CG_XK-step cycle (phase i in cg_pb[i])
     DBuf<CgState> cst;
     int cg_parity = 0;
     bool cg_ready = false;         // lsq_iterate state initialised (CG)
