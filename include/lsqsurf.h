@@ -234,9 +234,9 @@ int lsq_set_band_order(lsq_handle* h, int64_t n, const int32_t* perm);
  * equilibrated and factored inside its band (64×64 tiles, f64 MFMA); the rows of R⁻¹ needed are
  * formed by banded forward sweeps (never stored).  E[c] = sqrt(((AᵀA)⁻¹)_cc) per compact column.
  * For the n_ops rows of the CSR op (op_ptr[n_ops+1], op_col = compact columns, op_val):
- * op_err[i] = sqrt(op_i (AᵀA)⁻¹ op_iᵀ).  info (nullable, 4): band width in 64-column tiles, tile
- * rows, device bytes, 64×64 tile products of the sweeps.  Error -2 when the band does not fit the
- * device's free memory. */
+ * op_err[i] = sqrt(op_i (AᵀA)⁻¹ op_iᵀ).  info (nullable, 6): band width in 64-column tiles, tile
+ * rows, device bytes, 64×64 tile products of the sweeps, µs of the factorization and of the
+ * sweeps (host wall clock).  Error -2 when the band does not fit the device's free memory. */
 int lsq_cov_band(lsq_handle* h, const int32_t* perm, double* E, int64_t n_ops, const int64_t* op_ptr,
                  const int32_t* op_col, const double* op_val, double* op_err, int64_t* info);
 

@@ -23,6 +23,7 @@
 // storage n·(w+1)·64 doubles.  Takahashi's recurrence for the band of (AᵀA)⁻¹ costs only
 // ~T(w+1)² but its sums cancel in proportion to cond(AᵀA): measured 3e-6 relative at 48²×12,
 // 2 % at 64²×12 and negative diagonals beyond — so it is not used.
+#include <chrono>
 #include <algorithm>
 #include <climits>
 #include <cmath>
@@ -952,8 +953,10 @@ void band_cov(System& S, const int32_t* h_perm, int64_t nw, double* h_E, int64_t
     for (int64_t i = 0; i < nops; ++i)
         for (int64_t e = h_rp[i]; e < h_rp[i + 1]; ++e)
             if (h_ci[e] < 0 || h_ci[e] >= ncol) throw std::invalid_argument("lsq_cov_band: op column out of range");
+    const auto t0 = std::chrono::steady_clock::now();
     BandFactor F;
     band_factor(S, h_perm, F, nw);
+    const auto t1 = std::chrono::steady_clock::now();
     const int64_t n = F.n, T = F.T, npad = T * TB;
     const int w = F.w;
     std::vector<int32_t> pinv(ncol, -1);
@@ -1038,6 +1041,8 @@ void band_cov(System& S, const int32_t* h_perm, int64_t nw, double* h_E, int64_t
         info[1] = T;
         info[2] = bytes + ring.n * (int64_t)sizeof(double);
         info[3] = products;
+        info[4] = std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();   // factor (host wall)
+        info[5] = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t1).count();
     }
 }
 

@@ -26,6 +26,7 @@ its band on the device (lsq_cov_band_window); the averaging operators' rows go w
 their support's centre (their support must lie inside the window).  Accuracy against the full
 band factor: DESIGN.md §Error propagation (tests/test_gpu_errors_window.py).
 """
+import os
 from time import time
 
 import numpy as np
@@ -122,7 +123,11 @@ def window_cov(solver, grids, keep_cols, op=None, tile=WINDOW_TILE, margin=WINDO
         """inner: bool per window position (σ kept there, only their tiles swept) or None"""
         sub = op[rows] if rows is not None and rows.size else None
         cols = order[pos]
+        tc = time()
         Et, oe, info = solver.cov_band_window(cols, sub, inner=inner if inner is not None else np.zeros(pos.size, bool))
+        tsum[0] += time() - tc
+        tsum[1] += info[4] * 1e-6
+        tsum[2] += info[5] * 1e-6
         if inner is not None:
             E[cols[inner]] = Et[inner]
         if sub is not None:
@@ -131,6 +136,8 @@ def window_cov(solver, grids, keep_cols, op=None, tile=WINDOW_TILE, margin=WINDO
 
     ntiles = nown = 0
     wmax = products = 0
+    tsum = [0.0, 0.0, 0.0]   # seconds: inside lsq_cov_band_window, its factorizations, its sweeps
+    t_all = time()
     for ty in range(0, ny, tile):
         for tx in range(0, nx, tile):
             pos = window(ty - margin, ty + tile + margin, tx - margin, tx + tile + margin)
@@ -163,7 +170,8 @@ def window_cov(solver, grids, keep_cols, op=None, tile=WINDOW_TILE, margin=WINDO
     if timing is not None:
         timing['E_window'] = {'tiles': ntiles, 'op_windows': nown, 'tile': tile, 'margin': margin,
                               'max_band_tiles': wmax, 'tile_products': products, 'selfcheck_rel': check,
-                              'selfcheck_margin': m2}
+                              'selfcheck_margin': m2, 'time_s': time() - t_all, 'native_s': tsum[0],
+                              'factor_s': tsum[1], 'sweep_s': tsum[2]}
     return E, op_err, check
 
 
@@ -202,11 +210,13 @@ def calc_and_parse_errors(E, G_data, Gc, Ed, Ec, data, in_TSE, keep_cols, grids,
             keys = list(avg_ops)
             mats = [_compact_rows(avg_ops[k], keep_cols, Gc.col_N) for k in keys]
             op = sp.vstack(mats).tocsr() if mats else None
-            margin = WINDOW_MARGIN
+            # LSQ_E_TILE / LSQ_E_MARGIN: development overrides (A/B of the window geometry)
+            tile = int(os.environ.get('LSQ_E_TILE', WINDOW_TILE))
+            margin = m0 = int(os.environ.get('LSQ_E_MARGIN', WINDOW_MARGIN))
             while True:
-                E0c, errs, check = window_cov(fs.solver, grids, keep_cols, op, tile=WINDOW_TILE, margin=margin,
+                E0c, errs, check = window_cov(fs.solver, grids, keep_cols, op, tile=tile, margin=margin,
                                               timing=timing)
-                if check <= WINDOW_CHECK_TOL or margin >= 4 * WINDOW_MARGIN:
+                if check <= WINDOW_CHECK_TOL or margin >= 4 * m0:
                     break
                 print(f'calc_and_parse_errors: window sigma moved by {check:.1e} with twice the margin '
                       f'({margin} nodes); retrying with a margin of {2 * margin}', flush=True)
@@ -214,7 +224,7 @@ def calc_and_parse_errors(E, G_data, Gc, Ed, Ec, data, in_TSE, keep_cols, grids,
             if check > WINDOW_CHECK_TOL:
                 print(f'calc_and_parse_errors: WARNING window sigma within {check:.1e} only (margin {margin} nodes)',
                       flush=True)
-            approx = (f'window (conditional variance): tile {WINDOW_TILE}, margin {margin} nodes, '
+            approx = (f'window (conditional variance): tile {tile}, margin {margin} nodes, '
                       f'self-check {check:.1e} relative at twice the margin')
             timing['decompose_qz'] = time() - tic
             off = 0

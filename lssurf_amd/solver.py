@@ -291,7 +291,7 @@ class LSQSolver:
         the compact columns), sqrt(diag(op (AᵀA)⁻¹ opᵀ)).  `perm` (new position -> compact column)
         should make AᵀA banded (lsq_cov_band)."""
         E = np.zeros(self.n)
-        info = np.zeros(4, np.int64)
+        info = np.zeros(6, np.int64)
         pp = None if perm is None else as_c(perm, np.int32)
         if pp is not None and pp.size != self.n:
             raise ValueError('cov_band: perm must have one entry per column')
@@ -314,7 +314,7 @@ class LSQSolver:
         only the tiles holding those positions are swept; E is 0 elsewhere."""
         pp = as_c(perm_w, np.int32)
         E = np.zeros(pp.size)
-        info = np.zeros(4, np.int64)
+        info = np.zeros(6, np.int64)
         ii = None if inner is None else as_c(np.asarray(inner, dtype=bool), np.uint8)
         if ii is not None and ii.size != pp.size:
             raise ValueError('cov_band_window: inner must have one flag per window position')

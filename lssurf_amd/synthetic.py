@@ -28,6 +28,8 @@ CONFIGS = {
     # the per-rank compute floor of the strong-scaling runs, measurable on one GPU
     'c4y4': (1024, 12, 500_000, 258),
     'c4y8': (1024, 12, 250_000, 130),
+    # one rank's window of C5 (2048²×12, 8 M points) over 8 GPUs: 256 owned rows + 2 halo rows
+    'c5y8': (2048, 12, 1_000_000, 258),
     # anisotropic-constraint systems (BASELINE config C5: lssurf_amd.aniso.system3d — the z0
     # constraints are the notebook's directional operator along a circular field + magnitude)
     'c5a': (2048, 12, 8_000_000),
@@ -43,7 +45,7 @@ CONFIGS = {
 # inserting 't128' moved every later config onto new points (C5a: 61 → 72 multigrid iterations
 # between two builds that solve the same system alike).  New configs take new ids.
 SEED_ID = {'c1': 0, 'c3': 1, 'c4': 2, 'c5': 3, 't64': 4, 't256': 5, 't128': 6, 'tdense': 7, 't15': 8,
-           'c4y4': 9, 'c4y8': 10, 'c5a': 11, 'ta64': 12, 'ta100': 13, 't64z': 14, 'c3z': 15}
+           'c4y4': 9, 'c4y8': 10, 'c5a': 11, 'ta64': 12, 'ta100': 13, 't64z': 14, 'c3z': 15, 'c5y8': 16}
 ANISO = ('c5a', 'ta64', 'ta100')
 Z0_REFINED = ('t64z', 'c3z')
 

@@ -183,15 +183,15 @@ def test_window_node_blocks_cover_window_in_global_order(nranks):
     assert any(len(v) > 1 for v in seen.values())             # halo nodes are shared
 
 
-@pytest.mark.parametrize('name,nranks', [('c4y4', 4), ('c4y8', 8)])
-def test_slab_configs_are_one_rank_window_of_c4(name, nranks):
-    """synthetic 'c4y4' / 'c4y8' (the per-rank compute floor of bench --gpus 4 / 8):
-    the node-row count of one interior rank's window of C4 (owned rows + halo rows), C4's row
-    width, epochs and spacing, and 1/N of C4's points."""
+@pytest.mark.parametrize('name,nranks,base', [('c4y4', 4, 'c4'), ('c4y8', 8, 'c4'), ('c5y8', 8, 'c5')])
+def test_slab_configs_are_one_rank_window_of_c4(name, nranks, base):
+    """synthetic 'c4y4' / 'c4y8' / 'c5y8' (the per-rank compute floor of bench --gpus 4 / 8 on C4
+    and C5): the node-row count of one interior rank's window (owned rows + halo
+    rows), the full config's row width, epochs and spacing, and 1/N of its points."""
     from lssurf_amd import synthetic
-    n, nt, npts = synthetic.CONFIGS['c4']
+    n, nt, npts = synthetic.CONFIGS[base]
     kw, pts = synthetic.config_kwargs(name)
-    ck, cpts = synthetic.config_kwargs('c4')
+    ck, cpts = synthetic.config_kwargs(base)
     assert pts * nranks == cpts and kw['spacing'] == ck['spacing'] and kw['W']['x'] == ck['W']['x']
     ny = int(round(kw['W']['y'] / kw['spacing']['dz'])) + 1
     halo = 1   # one ghost node row per side (the stencils and the interpolation reach one row)
