@@ -253,6 +253,16 @@ int lsq_cov_band_window(lsq_handle* h, const int32_t* perm, int64_t n_win, const
                         int64_t n_ops, const int64_t* op_ptr, const int32_t* op_col, const double* op_val,
                         double* op_err, int64_t* info);
 
+/* Many windows at once (compute_E at scale): window w is perm[win_ptr[w] .. win_ptr[w+1]) with its
+ * inner flags and E (window order) at the same positions, and the op rows [win_ops[w],
+ * win_ops[w+1]) of the CSR op (op_ptr, op_pos = POSITIONS in window w, op_val; win_ops nullable:
+ * none) with op_err per row.  Windows are independent: they run on LSQ_E_LANES (default 3) stream
+ * lanes, one window's factorization (a latency-bound chain of tile steps) beside another's sweeps.
+ * info (nullable, 6): widest band, most tile rows, device bytes, tile products, µs, lanes. */
+int lsq_cov_band_windows(lsq_handle* h, int64_t n_windows, const int64_t* win_ptr, const int32_t* perm,
+                         const uint8_t* inner, double* E, const int64_t* win_ops, const int64_t* op_ptr,
+                         const int32_t* op_pos, const double* op_val, double* op_err, int64_t* info);
+
 /* The banded factor itself (replaces sparseqr.rz's R and E, smooth_fit.py:218 / the aniso notebook):
  * for the current weighted, masked A and the column order perm (nullable = natural),
  * (A·P)ᵀ(A·P) = RᵀR with R = R̃·S⁻¹, R̃ the upper band factor of the equilibrated S·Pᵀ(AᵀA)P·S.

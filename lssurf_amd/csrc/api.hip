@@ -634,6 +634,21 @@ int lsq_cov_band_window(lsq_handle* h, const int32_t* perm, int64_t n_win, const
     });
 }
 
+int lsq_cov_band_windows(lsq_handle* h, int64_t n_windows, const int64_t* win_ptr, const int32_t* perm,
+                         const uint8_t* inner, double* E, const int64_t* win_ops, const int64_t* op_ptr,
+                         const int32_t* op_pos, const double* op_val, double* op_err, int64_t* info) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_cov_band_windows: no matrix");
+        if (S.dist) return fail(S, "lsq_cov_band_windows: not available on distributed handles");
+        if (n_windows < 1 || !win_ptr || !perm || !E || win_ptr[0] != 0)
+            return fail(S, "lsq_cov_band_windows: bad windows");
+        if (win_ops && (!op_ptr || !op_err || (op_ptr[win_ops[n_windows]] > 0 && (!op_pos || !op_val))))
+            return fail(S, "lsq_cov_band_windows: bad op rows");
+        lsq::band_cov_windows(S, n_windows, win_ptr, perm, inner, E, win_ops, op_ptr, op_pos, op_val, op_err, info);
+        return 0;
+    });
+}
+
 int lsq_dist_set_global(lsq_handle* h, int64_t n_full, int32_t n_grids, const lsq_grid_desc* grids, int32_t n_stencil,
                         const lsq_stencil_desc* stencils, const int32_t* local_of, int32_t win_row0, int32_t own_row0,
                         int32_t own_row1, int32_t rows) {

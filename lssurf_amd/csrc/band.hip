@@ -714,15 +714,16 @@ struct SweepOps {
     int64_t gemms = 0;
 };
 
+// pinv: compact column -> position (null: ci already holds positions)
 SweepOps sweep_ops(const std::vector<int64_t>& rows, const int64_t* rp, const int32_t* ci, const double* v,
-                   const std::vector<int32_t>& pinv, int64_t T, int w) {
+                   const int32_t* pinv, int64_t T, int w) {
     SweepOps o;
     struct Ent { int64_t K; int32_t p; double v; };
     for (size_t r0 = 0; r0 < rows.size(); r0 += TB) {
         std::vector<Ent> ents;
         for (size_t q = r0; q < std::min(rows.size(), r0 + TB); ++q)
             for (int64_t e = rp[rows[q]]; e < rp[rows[q] + 1]; ++e) {
-                const int64_t j = pinv[ci[e]];
+                const int64_t j = pinv ? pinv[ci[e]] : ci[e];
                 ents.push_back({j >> 6, (int32_t)(((j & 63) << 6) | (int64_t)(q - r0)), v[e]});
             }
         std::stable_sort(ents.begin(), ents.end(), [](const Ent& a, const Ent& b) { return a.K < b.K; });
@@ -740,6 +741,38 @@ SweepOps sweep_ops(const std::vector<int64_t>& rows, const int64_t* rp, const in
         o.gemms += (T - ents.front().K) * (int64_t)(w + 1);
     }
     return o;
+}
+
+// The tile steps of the band Cholesky, asynchronous on st (+ side): look-ahead — step K's POTRF,
+// TRSM and next-row update on st; the rest of its trailing update (rows K+2..) on side, joined
+// before the next-row update of K+1; then D_K = R_KK⁻¹ for every tile row.  err: non-positive pivot.
+void band_factor_steps(const BandDev& b, hipStream_t st, hipStream_t side, hipEvent_t fork, hipEvent_t join, int* err) {
+    const int64_t T = b.T;
+    const int w = b.w;
+    HIP_CHECK(hipEventRecord(join, st));
+    for (int64_t K = 0; K < T; ++K) {
+        hipLaunchKernelGGL(k_band_potrf, dim3(1), dim3(BLOCK), 0, st, b, K, err);
+        const int m = (int)std::min<int64_t>(w, T - 1 - K);
+        if (m > 0) {
+            hipLaunchKernelGGL(k_band_trsm, dim3(m), dim3(BLOCK), 0, st, b, K);
+            HIP_CHECK(hipStreamWaitEvent(st, join, 0));
+            hipLaunchKernelGGL(k_band_syrk<true>, dim3(m), dim3(BLOCK), 0, st, b, K, m);
+            if (m > 1) {
+                HIP_CHECK(hipEventRecord(fork, st));
+                HIP_CHECK(hipStreamWaitEvent(side, fork, 0));
+                hipLaunchKernelGGL(k_band_syrk<false>, dim3((m - 1) * m / 2), dim3(BLOCK), 0, side, b, K, m);
+                HIP_CHECK(hipEventRecord(join, side));
+            }
+        }
+    }
+    HIP_CHECK(hipStreamWaitEvent(st, join, 0));
+    hipLaunchKernelGGL(k_band_dinv, dim3((unsigned)T), dim3(TB), 0, st, b);
+    KERNEL_CHECK();
+}
+
+__global__ __launch_bounds__(BLOCK) void k_band_pinv(int64_t n, const int32_t* __restrict__ perm,
+                                                     int32_t* __restrict__ pinv) {
+    for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLOCK) pinv[perm[j]] = (int32_t)j;
 }
 
 // launch the sweeps of `nwg` workgroups in batches whose rings fit `ring` (cap workgroups each)
@@ -823,27 +856,7 @@ void band_factor(System& S, const int32_t* h_perm, BandFactor& F, int64_t nw) {
         HIP_CHECK(hipEventCreateWithFlags(&S.ev_fork, hipEventDisableTiming));
         HIP_CHECK(hipEventCreateWithFlags(&S.ev_join, hipEventDisableTiming));
     }
-    // look-ahead: step K's POTRF, TRSM and next-row update on the main stream; the rest of its
-    // trailing update (rows K+2..) on the side stream, joined before the next-row update of K+1
-    HIP_CHECK(hipEventRecord(S.ev_join, st));
-    for (int64_t K = 0; K < T; ++K) {
-        hipLaunchKernelGGL(k_band_potrf, dim3(1), dim3(BLOCK), 0, st, b, K, err.p);
-        const int m = (int)std::min<int64_t>(w, T - 1 - K);
-        if (m > 0) {
-            hipLaunchKernelGGL(k_band_trsm, dim3(m), dim3(BLOCK), 0, st, b, K);
-            HIP_CHECK(hipStreamWaitEvent(st, S.ev_join, 0));
-            hipLaunchKernelGGL(k_band_syrk<true>, dim3(m), dim3(BLOCK), 0, st, b, K, m);
-            if (m > 1) {
-                HIP_CHECK(hipEventRecord(S.ev_fork, st));
-                HIP_CHECK(hipStreamWaitEvent(S.side, S.ev_fork, 0));
-                hipLaunchKernelGGL(k_band_syrk<false>, dim3((m - 1) * m / 2), dim3(BLOCK), 0, S.side, b, K, m);
-                HIP_CHECK(hipEventRecord(S.ev_join, S.side));
-            }
-        }
-    }
-    HIP_CHECK(hipStreamWaitEvent(st, S.ev_join, 0));
-    hipLaunchKernelGGL(k_band_dinv, dim3((unsigned)T), dim3(TB), 0, st, b);
-    KERNEL_CHECK();
+    band_factor_steps(b, st, S.side, S.ev_fork, S.ev_join, err.p);
     int h_err = 0;
     HIP_CHECK(hipMemcpyAsync(&h_err, err.p, sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
@@ -1018,7 +1031,7 @@ void band_cov(System& S, const int32_t* h_perm, int64_t nw, double* h_E, int64_t
     if (nops > 0) {
         std::vector<int64_t> rows(nops);
         for (int64_t i = 0; i < nops; ++i) rows[i] = i;
-        SweepOps so = sweep_ops(rows, h_rp, h_ci, h_v, pinv, T, w);
+        SweepOps so = sweep_ops(rows, h_rp, h_ci, h_v, pinv.data(), T, w);
         products += so.gemms;
         const int64_t nwg = (int64_t)so.sp.size() - 1;
         DBuf<int64_t> dsp(nwg + 1), dsegK((int64_t)so.segK.size()), dsegE((int64_t)so.segE.size());
@@ -1043,6 +1056,216 @@ void band_cov(System& S, const int32_t* h_perm, int64_t nw, double* h_E, int64_t
         info[3] = products;
         info[4] = std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();   // factor (host wall)
         info[5] = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t1).count();
+    }
+}
+
+
+// ---- many windows, pipelined (lsq_cov_band_windows) ------------------------------------------
+// compute_E at scale factors hundreds of windows.  One window's factorization is a chain of T
+// dependent tile steps of 1–w workgroups (latency-bound: the GPU is mostly idle), and its interior
+// sweeps fill the chip only partly.  Windows are independent, so they run on NL lanes — each lane
+// its own stream pair and persistent buffers (no allocation or free per window: hipFree would
+// synchronise the device) — so window i + 1's factorization overlaps window i's sweeps.  The host
+// waits for a lane only before reusing it.
+namespace {
+struct BandLane {
+    hipStream_t st = nullptr, side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    DBuf<double> R, D, sc, ring, ssq, dE, dout, ev;
+    DBuf<int32_t> perm, pinv, el;
+    DBuf<int64_t> tiles, sp, segK, segE;
+    DBuf<int> wmax, err;
+    double *hE = nullptr, *hout = nullptr;
+    int* herr = nullptr;
+    int64_t capE = 0, capOut = 0;
+    // the window whose results are in flight on this lane
+    int64_t win = -1, n = 0, nops = 0;
+    double* E = nullptr;
+    double* op_err = nullptr;
+    const uint8_t* inner = nullptr;
+    ~BandLane() {
+        if (hE) (void)hipHostFree(hE);
+        if (hout) (void)hipHostFree(hout);
+        if (herr) (void)hipHostFree(herr);
+        if (fork) (void)hipEventDestroy(fork);
+        if (join) (void)hipEventDestroy(join);
+        if (st) (void)hipStreamDestroy(st);
+        if (side) (void)hipStreamDestroy(side);
+    }
+};
+template <class T>
+void grow(DBuf<T>& b, int64_t n) {
+    if (b.n < n) b.alloc(n);
+}
+// results of the lane's window in flight: wait, copy out, check the factor
+void lane_finish(BandLane& L) {
+    if (L.win < 0) return;
+    HIP_CHECK(hipStreamSynchronize(L.st));
+    if (*L.herr) throw std::invalid_argument("lsq_cov_band_windows: AᵀA of window " + std::to_string(L.win) +
+                                             " is not positive definite (rank-deficient system)");
+    for (int64_t j = 0; j < L.n; ++j) L.E[j] = (!L.inner || L.inner[j]) ? L.hE[j] : 0.0;
+    for (int64_t i = 0; i < L.nops; ++i) L.op_err[i] = std::sqrt(L.hout[i]);
+    L.win = -1;
+}
+}  // namespace
+
+void band_cov_windows(System& S, int64_t nwin, const int64_t* win_ptr, const int32_t* h_perm, const uint8_t* inner,
+                      double* h_E, const int64_t* win_ops, const int64_t* op_ptr, const int32_t* op_pos,
+                      const double* op_val, double* op_err, int64_t* info) {
+    refresh_scaling(S, S.cs_mode < 0 ? 0 : S.cs_mode);
+    ensure_full_csr(S);   // the band of AᵀA from G / GT
+    const int64_t ncol = S.G.n;
+    int64_t nmax = 0, omax = 0;
+    for (int64_t w = 0; w < nwin; ++w) {
+        const int64_t n = win_ptr[w + 1] - win_ptr[w];
+        if (n < 1 || n > ncol) throw std::invalid_argument("lsq_cov_band_windows: bad window");
+        nmax = std::max(nmax, n);
+        if (win_ops) omax = std::max(omax, win_ops[w + 1] - win_ops[w]);
+        for (int64_t j = win_ptr[w]; j < win_ptr[w + 1]; ++j)
+            if (h_perm[j] < 0 || h_perm[j] >= ncol) throw std::invalid_argument("lsq_cov_band_windows: column out of range");
+        if (win_ops)
+            for (int64_t i = win_ops[w]; i < win_ops[w + 1]; ++i)
+                for (int64_t e = op_ptr[i]; e < op_ptr[i + 1]; ++e)
+                    if (op_pos[e] < 0 || op_pos[e] >= n)
+                        throw std::invalid_argument("lsq_cov_band_windows: an op row reaches outside its window");
+    }
+    const int nl = [] {
+        const char* e = getenv("LSQ_E_LANES");
+        return e ? std::max(1, std::min(atoi(e), 8)) : 3;
+    }();
+    std::vector<BandLane> lanes(nl);
+    const int64_t nopad = (omax + TB - 1) / TB * TB;
+    for (BandLane& L : lanes) {
+        HIP_CHECK(hipStreamCreateWithFlags(&L.st, hipStreamNonBlocking));
+        HIP_CHECK(hipStreamCreateWithFlags(&L.side, hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&L.fork, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&L.join, hipEventDisableTiming));
+        HIP_CHECK(hipHostMalloc(&L.hE, sizeof(double) * std::max<int64_t>(nmax, 1)));
+        HIP_CHECK(hipHostMalloc(&L.hout, sizeof(double) * std::max<int64_t>(nopad, 1)));
+        HIP_CHECK(hipHostMalloc(&L.herr, sizeof(int)));
+        L.pinv.alloc(ncol);
+        L.wmax.alloc(1);
+        L.err.alloc(1);
+    }
+    HIP_CHECK(hipStreamSynchronize(S.stream));   // formation / scaling done before the lanes read them
+    int64_t products = 0, wmax_all = 0, tmax = 0, dev_bytes = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    try {
+        for (int64_t w = 0; w < nwin; ++w) {
+            BandLane& L = lanes[w % nl];
+            lane_finish(L);
+            const int64_t n = win_ptr[w + 1] - win_ptr[w], T = (n + TB - 1) / TB, npad = T * TB;
+            const int32_t* perm = h_perm + win_ptr[w];
+            const uint8_t* inw = inner ? inner + win_ptr[w] : nullptr;
+            hipStream_t st = L.st;
+            // the window's order on the device and its inverse over every compact column (−1 outside)
+            grow(L.perm, n);
+            L.perm.upload(perm, n, st);
+            HIP_CHECK(hipMemsetAsync(L.pinv.p, 0xff, sizeof(int32_t) * ncol, st));
+            hipLaunchKernelGGL(k_band_pinv, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, L.perm.p, L.pinv.p);
+            L.wmax.zero(st);
+            hipLaunchKernelGGL(k_band_width, dim3(grid_for(S.G.m)), dim3(BLOCK), 0, st, S.G.m, S.G.rp.p, S.G.ci.p,
+                               L.pinv.p, S.rs.p, L.wmax.p);
+            KERNEL_CHECK();
+            int hw = 0;
+            HIP_CHECK(hipMemcpyAsync(&hw, L.wmax.p, sizeof(int), hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));   // this lane only: the others keep running
+            const int bw = (int)std::min<int64_t>(hw, T - 1);
+            const int64_t band_tiles = T * (int64_t)(bw + 1);
+            // the interior's tiles (the sweeps) and the op rows' sweep plan (positions: no pinv)
+            std::vector<int64_t> tiles;
+            for (int64_t J = 0; J < T; ++J) {
+                bool any = !inw;
+                for (int64_t j = J * TB; j < std::min<int64_t>(n, (J + 1) * TB) && !any; ++j) any = inw[j] != 0;
+                if (any) tiles.push_back(J);
+            }
+            const int64_t nops = win_ops ? win_ops[w + 1] - win_ops[w] : 0;
+            SweepOps so;
+            if (nops > 0) {
+                std::vector<int64_t> rows(nops);
+                for (int64_t i = 0; i < nops; ++i) rows[i] = win_ops[w] + i;
+                so = sweep_ops(rows, op_ptr, op_pos, op_val, nullptr, T, bw);
+            }
+            const int64_t nsw = (int64_t)tiles.size(), nopw = nops > 0 ? (int64_t)so.sp.size() - 1 : 0;
+            for (int64_t J : tiles) products += (T - J) * (int64_t)std::min<int64_t>(bw + 1, T - J);
+            products += so.gemms;
+            const int64_t cap = std::max<int64_t>({nsw, nopw, 1});
+            const int64_t need = (band_tiles + T + cap * (bw + 1)) * TT * (int64_t)sizeof(double);
+            if (L.R.n < band_tiles * TT || L.ring.n < cap * (bw + 1) * TT) {
+                size_t free_b = 0, total_b = 0;
+                HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+                if ((double)need > 0.8 * (double)free_b)
+                    throw Refused("lsq_cov_band_windows: a window band of " + std::to_string(bw) +
+                                  " tiles and its sweeps need " + std::to_string(need >> 20) +
+                                  " MiB, more than the device has free (fewer lanes: LSQ_E_LANES)");
+            }
+            grow(L.R, band_tiles * TT);
+            grow(L.D, T * TT);
+            grow(L.sc, npad);
+            grow(L.ssq, npad);
+            grow(L.dE, n);
+            grow(L.ring, cap * (bw + 1) * TT);
+            dev_bytes = std::max<int64_t>(dev_bytes, nl * need);
+            wmax_all = std::max<int64_t>(wmax_all, bw);
+            tmax = std::max(tmax, T);
+            HIP_CHECK(hipMemsetAsync(L.R.p, 0, sizeof(double) * band_tiles * TT, st));
+            BandDev b{T, bw, L.R.p, L.D.p};
+            hipLaunchKernelGGL(k_band_normal, dim3(grid_for(npad)), dim3(BLOCK), 0, st, n, npad, b, L.perm.p, L.pinv.p,
+                               S.GT.rp.p, S.GT.ci.p, S.GT.val.p, S.G.rp.p, S.G.ci.p, S.G.val.p, S.rs.p);
+            hipLaunchKernelGGL(k_band_dscale, dim3(grid_for(npad)), dim3(BLOCK), 0, st, b, npad, L.sc.p);
+            hipLaunchKernelGGL(k_band_apply_scale, dim3(grid_for(band_tiles * TT)), dim3(BLOCK), 0, st, b, L.sc.p);
+            KERNEL_CHECK();
+            L.err.zero(st);
+            band_factor_steps(b, st, L.side, L.fork, L.join, L.err.p);
+            HIP_CHECK(hipMemcpyAsync(L.herr, L.err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+            // the diagonal over the interior's tiles, E in window order
+            HIP_CHECK(hipMemsetAsync(L.ssq.p, 0, sizeof(double) * npad, st));
+            if (nsw > 0) {
+                grow(L.tiles, nsw);
+                L.tiles.upload(tiles.data(), nsw, st);
+                run_sweeps<true>(st, b, nsw, cap, L.tiles.p, nullptr, nullptr, nullptr, nullptr, L.sc.p, L.ring.p,
+                                 L.ssq.p);
+            }
+            hipLaunchKernelGGL(k_band_diag_sweep, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, nullptr, L.ssq.p, L.sc.p,
+                               L.dE.p);
+            KERNEL_CHECK();
+            HIP_CHECK(hipMemcpyAsync(L.hE, L.dE.p, sizeof(double) * n, hipMemcpyDeviceToHost, st));
+            if (nops > 0) {   // the op rows' errors
+                grow(L.sp, nopw + 1);
+                grow(L.segK, (int64_t)so.segK.size());
+                grow(L.segE, (int64_t)so.segE.size());
+                grow(L.el, std::max<int64_t>((int64_t)so.el.size(), 1));
+                grow(L.ev, std::max<int64_t>((int64_t)so.ev.size(), 1));
+                grow(L.dout, nopw * TB);
+                L.sp.upload(so.sp.data(), nopw + 1, st);
+                L.segK.upload(so.segK.data(), (int64_t)so.segK.size(), st);
+                L.segE.upload(so.segE.data(), (int64_t)so.segE.size(), st);
+                L.el.upload(so.el.data(), (int64_t)so.el.size(), st);
+                L.ev.upload(so.ev.data(), (int64_t)so.ev.size(), st);
+                run_sweeps<false>(st, b, nopw, cap, L.sp.p, L.segK.p, L.segE.p, L.el.p, L.ev.p, L.sc.p, L.ring.p,
+                                  L.dout.p);
+                HIP_CHECK(hipMemcpyAsync(L.hout, L.dout.p, sizeof(double) * nops, hipMemcpyDeviceToHost, st));
+            }
+            L.win = w;
+            L.n = n;
+            L.nops = nops;
+            L.E = h_E + win_ptr[w];
+            L.op_err = nops > 0 ? op_err + win_ops[w] : nullptr;
+            L.inner = inw;
+        }
+        for (BandLane& L : lanes) lane_finish(L);
+    } catch (...) {
+        for (BandLane& L : lanes)
+            if (L.st) (void)hipStreamSynchronize(L.st);
+        throw;
+    }
+    if (info) {
+        info[0] = wmax_all;
+        info[1] = tmax;
+        info[2] = dev_bytes;
+        info[3] = products;
+        info[4] = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+        info[5] = nl;
     }
 }
 

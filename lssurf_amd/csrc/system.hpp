@@ -542,7 +542,11 @@ void band_factor_download(System& S, const int32_t* perm, int64_t* info, double*
 // nw ≥ 0 (a window): E in window order (nw entries); inner (nullable): the window positions whose
 // tiles are swept (E 0 elsewhere).  nw < 0: E over every compact column.
 void band_cov(System& S, const int32_t* perm, int64_t nw, double* E, int64_t nops, const int64_t* rp, const int32_t* ci,
-              const double* v, double* op_err, int64_t* info, const uint8_t* inner = nullptr);   // rs/cs -> SELL values (single GPU)
+              const double* v, double* op_err, int64_t* info, const uint8_t* inner = nullptr);
+// many windows, pipelined over lanes (lsq_cov_band_windows)
+void band_cov_windows(System& S, int64_t nwin, const int64_t* win_ptr, const int32_t* perm, const uint8_t* inner,
+                      double* E, const int64_t* win_ops, const int64_t* op_ptr, const int32_t* op_pos,
+                      const double* op_val, double* op_err, int64_t* info);   // rs/cs -> SELL values (single GPU)
 void scaling_rows_colnorm(System& S, int precond, bool raw);
 void mf_column_scale(System& S, bool raw);       // lsqr.hip: column norms from the stencil structure
 void scaling_finish_cs(System& S);

@@ -56,6 +56,7 @@ def band_order(grids, keep_cols):
 
 WINDOW_MIN_COLS = 250_000      # 'auto': the full band below, tiled windows above
 WINDOW_TILE, WINDOW_MARGIN = 64, 24   # σ within ~3e-6 of the full band at 128²×12 (tests)
+WINDOW_BATCH = 64              # windows per lsq_cov_band_windows call (host memory of their column lists)
 WINDOW_CHECK_TOL = 1e-4        # self-check bound: σ of a sample tile at twice the margin (the margin
                                # doubles, up to 4×, until it holds; the reference's own Rinv
                                # truncation moves σ by ~1e-5)
@@ -119,50 +120,52 @@ def window_cov(solver, grids, keep_cols, op=None, tile=WINDOW_TILE, margin=WINDO
             m &= (yy >= y0) & (yy < y1)
         return a + np.flatnonzero(m)
 
-    def run(pos, inner, rows):
-        """inner: bool per window position (σ kept there, only their tiles swept) or None"""
-        sub = op[rows] if rows is not None and rows.size else None
-        cols = order[pos]
-        tc = time()
-        Et, oe, info = solver.cov_band_window(cols, sub, inner=inner if inner is not None else np.zeros(pos.size, bool))
-        tsum[0] += time() - tc
-        tsum[1] += info[4] * 1e-6
-        tsum[2] += info[5] * 1e-6
-        if inner is not None:
-            E[cols[inner]] = Et[inner]
-        if sub is not None:
-            op_err[rows] = oe
-        return int(info[0]), int(info[3])
-
-    ntiles = nown = 0
-    wmax = products = 0
-    tsum = [0.0, 0.0, 0.0]   # seconds: inside lsq_cov_band_window, its factorizations, its sweeps
-    t_all = time()
+    # every window (tile ± margin, the op rows of the tile's centre; op rows wider than that get a
+    # window of their own; last, the self-check: the most central tile with twice the margin), then
+    # the device runs them in chunks, several windows at a time (lsq_cov_band_windows)
+    wins = []   # (positions, inner flags or None, op rows or None)
     for ty in range(0, ny, tile):
         for tx in range(0, nx, tile):
             pos = window(ty - margin, ty + tile + margin, tx - margin, tx + tile + margin)
             yi, xi = iy_o[pos], ix_o[pos]
             inner = (yi >= ty) & (yi < ty + tile) & (xi >= tx) & (xi < tx + tile)
             rows = None if op is None else np.flatnonzero((oty == ty // tile) & (otx == tx // tile) & ~own)
-            w_, p_ = run(pos, inner, rows)
-            wmax, products = max(wmax, w_), products + p_
-            ntiles += 1
+            wins.append((pos, inner, rows))
+    ntiles = len(wins)
     if op is not None and own.any():   # one window per distinct support box
         boxes = np.stack([y_lo, y_hi, x_lo, x_hi], axis=1)
         for b in np.unique(boxes[own], axis=0):
             rows = np.flatnonzero(own & np.all(boxes == b, axis=1))
-            pos = window(b[0] - margin, b[1] + margin + 1, b[2] - margin, b[3] + margin + 1)
-            w_, p_ = run(pos, None, rows)
-            wmax, products = max(wmax, w_), products + p_
-            nown += 1
-    # self-check: the most central tile again with twice the margin; σ of its columns moves by the
-    # correlations the margin cut off (conditional vs marginal variance)
+            wins.append((window(b[0] - margin, b[1] + margin + 1, b[2] - margin, b[3] + margin + 1),
+                         None, rows))
+    nown = len(wins) - ntiles
     cy, cx = (ny // 2) // tile * tile, (nx // 2) // tile * tile
     m2 = 2 * margin
     pos2 = window(cy - m2, cy + tile + m2, cx - m2, cx + tile + m2)
     yi, xi = iy_o[pos2], ix_o[pos2]
     inner2 = (yi >= cy) & (yi < cy + tile) & (xi >= cx) & (xi < cx + tile)
-    E2, _, _ = solver.cov_band_window(order[pos2], None, inner=inner2)
+    wins.append((pos2, inner2, None))
+    E2 = None
+    wmax = products = 0
+    t_all = time()
+    batch = int(os.environ.get('LSQ_E_BATCH', WINDOW_BATCH))
+    for c0 in range(0, len(wins), max(batch, 1)):
+        chunk = wins[c0:c0 + max(batch, 1)]
+        req = [(order[pos], inner if inner is not None else np.zeros(pos.size, bool),
+                op[rows] if (op is not None and rows is not None and rows.size) else None)
+               for pos, inner, rows in chunk]
+        Es, oes, info = solver.cov_band_windows(req)
+        wmax, products = max(wmax, int(info[0])), products + int(info[3])
+        for k, ((pos, inner, rows), (cols, _, _), Et, oe) in enumerate(zip(chunk, req, Es, oes)):
+            if c0 + k == len(wins) - 1:       # the self-check window
+                E2 = Et
+                continue
+            if inner is not None:
+                E[cols[inner]] = Et[inner]
+            if oe is not None:
+                op_err[rows] = oe
+    # self-check: σ of the central tile's columns moves by the correlations the margin cut off
+    # (conditional vs marginal variance)
     c2 = order[pos2][inner2]
     e1, e2 = E[c2], E2[inner2]
     sel = e2 > 0
@@ -170,8 +173,8 @@ def window_cov(solver, grids, keep_cols, op=None, tile=WINDOW_TILE, margin=WINDO
     if timing is not None:
         timing['E_window'] = {'tiles': ntiles, 'op_windows': nown, 'tile': tile, 'margin': margin,
                               'max_band_tiles': wmax, 'tile_products': products, 'selfcheck_rel': check,
-                              'selfcheck_margin': m2, 'time_s': time() - t_all, 'native_s': tsum[0],
-                              'factor_s': tsum[1], 'sweep_s': tsum[2]}
+                              'selfcheck_margin': m2, 'time_s': time() - t_all, 'lanes': int(info[5]),
+                              'batch': batch}
     return E, op_err, check
 
 

@@ -330,6 +330,51 @@ class LSQSolver:
                                                 ptr(ci), ptr(v), ptr(out), ptr(info)), 'lsq_cov_band_window')
         return E, out, info
 
+    def cov_band_windows(self, windows):
+        """cov_band_window for many windows at once, pipelined on the device (lsq_cov_band_windows):
+        windows = [(perm_w, inner or None, op or None)] with op rows over the COMPACT columns, every
+        row inside its window.  Returns ([E_w (window order)], [op_err_w or None], info)."""
+        sizes = [len(w[0]) for w in windows]
+        wp = as_c(np.r_[0, np.cumsum(sizes)], np.int64)
+        perm = as_c(np.concatenate([np.asarray(w[0]) for w in windows]), np.int32)
+        inner = as_c(np.concatenate([np.ones(sz, bool) if w[1] is None else np.asarray(w[1], bool)
+                                     for w, sz in zip(windows, sizes)]), np.uint8)
+        E = np.zeros(perm.size)
+        info = np.zeros(6, np.int64)
+        ops = [w[2] for w in windows]
+        if all(o is None or o.shape[0] == 0 for o in ops):
+            self._check(self._L.lsq_cov_band_windows(self._h, len(windows), ptr(wp), ptr(perm), ptr(inner), ptr(E),
+                                                     None, None, None, None, None, ptr(info)), 'lsq_cov_band_windows')
+            return [E[wp[i]:wp[i + 1]] for i in range(len(windows))], [None] * len(windows), info
+        nrow = [0 if o is None else o.shape[0] for o in ops]
+        wo = as_c(np.r_[0, np.cumsum(nrow)], np.int64)
+        rps, poss, vals = [np.zeros(1, np.int64)], [], []
+        base = 0
+        pos_of = np.full(self.n, -1, np.int64)
+        for (cols, _, op), nr in zip(windows, nrow):
+            if not nr:
+                continue
+            op = sp.csr_matrix(op)
+            op.sort_indices()
+            pos_of[np.asarray(cols)] = np.arange(len(cols))
+            p = pos_of[op.indices]
+            pos_of[np.asarray(cols)] = -1
+            if p.size and p.min() < 0:
+                raise ValueError('cov_band_windows: an op row reaches outside its window')
+            rps.append(op.indptr[1:].astype(np.int64) + base)
+            base += op.indptr[-1]
+            poss.append(p)
+            vals.append(op.data)
+        rp = as_c(np.concatenate(rps), np.int64)
+        pos = as_c(np.concatenate(poss) if poss else np.zeros(0), np.int32)
+        val = as_c(np.concatenate(vals) if vals else np.zeros(0), np.float64)
+        oe = np.zeros(int(wo[-1]))
+        self._check(self._L.lsq_cov_band_windows(self._h, len(windows), ptr(wp), ptr(perm), ptr(inner), ptr(E),
+                                                 ptr(wo), ptr(rp), ptr(pos), ptr(val), ptr(oe), ptr(info)),
+                    'lsq_cov_band_windows')
+        return ([E[wp[i]:wp[i + 1]] for i in range(len(windows))],
+                [oe[wo[i]:wo[i + 1]] if nrow[i] else None for i in range(len(windows))], info)
+
     def spmv(self, x, trans=False):
         """G x (trans False) or Gᵀ x on the UNWEIGHTED formed operator, all rows."""
         x = as_c(x, np.float64)

@@ -114,3 +114,45 @@ def test_window_averaging_errors(gpu_available):
     for k in keys:
         E = getattr(S['E']['sigma_' + k], 'sigma_' + k)
         assert rel(E, g['Eexact_sigma_' + k]) < 1e-5, k
+
+
+@pytest.mark.parametrize('lanes', ['1', '3'])
+def test_batched_windows_equal_single_windows(gpu_available, lanes):
+    """lsq_cov_band_windows (windows pipelined over stream lanes, interior-only sweeps, op rows as
+    window positions) returns bit for bit what lsq_cov_band_window returns window by window: the
+    same kernels in the same order per window, whatever runs beside it."""
+    import os
+    import scipy.sparse as sp
+    from lssurf_amd.errors import band_order, _node_index
+    S, fs, keep = _system('t64')
+    saved = os.environ.get('LSQ_E_LANES')
+    os.environ['LSQ_E_LANES'] = lanes
+    try:
+        o = band_order(S['grids'], keep)
+        iy, ix = _node_index(S['grids'], keep)
+        iy_o, ix_o = iy[o], ix[o]
+        rng = np.random.default_rng(5)
+        wins = []
+        for (y0, x0) in [(0, 0), (16, 24), (40, 40), (8, 48)]:
+            sel = np.flatnonzero((iy_o >= y0) & (iy_o < y0 + 24) & (ix_o >= x0) & (ix_o < x0 + 16))
+            inner = (iy_o[sel] >= y0 + 4) & (iy_o[sel] < y0 + 20) & (ix_o[sel] >= x0 + 4) & (ix_o[sel] < x0 + 12)
+            cols = o[sel]
+            # op rows: pairs of the window's interior columns (as averaging operators' rows)
+            a = rng.choice(cols[inner], size=70)
+            b = rng.choice(cols[inner], size=70)
+            op = sp.csr_matrix((np.r_[np.full(70, 0.5), np.full(70, 0.5)], (np.r_[np.arange(70), np.arange(70)],
+                                np.r_[a, b])), shape=(70, keep.size))
+            wins.append((cols, inner, op))
+        Eb, ob, info = fs.solver.cov_band_windows(wins)
+        for (cols, inner, op), e, oe in zip(wins, Eb, ob):
+            es, oes, _ = fs.solver.cov_band_window(cols, op, inner=inner)
+            np.testing.assert_array_equal(e, es)
+            np.testing.assert_array_equal(oe, oes)
+            assert np.all(e[~inner] == 0.0) and np.all(e[inner] > 0.0)
+        assert int(info[5]) == int(lanes)
+    finally:
+        fs.close()
+        if saved is None:
+            os.environ.pop('LSQ_E_LANES', None)
+        else:
+            os.environ['LSQ_E_LANES'] = saved
