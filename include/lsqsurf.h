@@ -256,7 +256,7 @@ int lsq_cov_band_window(lsq_handle* h, const int32_t* perm, int64_t n_win, const
 /* Many windows at once (compute_E at scale): window w is perm[win_ptr[w] .. win_ptr[w+1]) with its
  * inner flags and E (window order) at the same positions, and the op rows [win_ops[w],
  * win_ops[w+1]) of the CSR op (op_ptr, op_pos = POSITIONS in window w, op_val; win_ops nullable:
- * none) with op_err per row.  Windows are independent: they run on LSQ_E_LANES (default 3) stream
+ * none) with op_err per row.  Windows are independent: they run on LSQ_E_LANES (default 2) stream
  * lanes, one window's factorization (a latency-bound chain of tile steps) beside another's sweeps.
  * info (nullable, 6): widest band, most tile rows, device bytes, tile products, µs, lanes. */
 int lsq_cov_band_windows(lsq_handle* h, int64_t n_windows, const int64_t* win_ptr, const int32_t* perm,

@@ -1131,7 +1131,7 @@ void band_cov_windows(System& S, int64_t nwin, const int64_t* win_ptr, const int
     }
     const int nl = [] {
         const char* e = getenv("LSQ_E_LANES");
-        return e ? std::max(1, std::min(atoi(e), 8)) : 3;
+        return e ? std::max(1, std::min(atoi(e), 8)) : 2;   // C4, 32-node tiles: 2 lanes 132 s, 4 lanes 134 s
     }();
     std::vector<BandLane> lanes(nl);
     const int64_t nopad = (omax + TB - 1) / TB * TB;

@@ -55,7 +55,11 @@ def band_order(grids, keep_cols):
 
 
 WINDOW_MIN_COLS = 250_000      # 'auto': the full band below, tiled windows above
-WINDOW_TILE, WINDOW_MARGIN = 64, 24   # σ within ~3e-6 of the full band at 128²×12 (tests)
+# tile 32 (round 5; 64 before): a window's interior sweeps cost ~(margin + tile/2)·(tile + 2·margin)²
+# per column, so 32-node tiles do 2.4× fewer tile products at C4 (4.2·10⁹ against 1.0·10¹⁰) for
+# 4× the windows, whose factorizations now run beside other windows' sweeps; σ within 3.5e-6 of
+# the full band at 256²×12 (64-node tiles: 1.7e-6), the same self-check at C4 (7.1e-7)
+WINDOW_TILE, WINDOW_MARGIN = 32, 24
 WINDOW_BATCH = 64              # windows per lsq_cov_band_windows call (host memory of their column lists)
 WINDOW_CHECK_TOL = 1e-4        # self-check bound: σ of a sample tile at twice the margin (the margin
                                # doubles, up to 4×, until it holds; the reference's own Rinv

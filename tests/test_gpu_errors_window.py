@@ -66,7 +66,7 @@ def test_window_covariance_matches_full_band(gpu_available, name, tile, margin, 
 
 
 def test_window_stiff_default_tile_and_self_check(gpu_available):
-    """The stiff E_RMS (correlations reach further) with the default tile / margin (64 / 24 nodes):
+    """The stiff E_RMS (correlations reach further) with the default tile / margin (32 / 24 nodes):
     the window σ against the full band, and the self-check window_cov reports (the most central tile
     again with twice the margin) bounds the error it measures to within an order of magnitude —
     calc_and_parse_errors grows the margin when the self-check exceeds WINDOW_CHECK_TOL."""
