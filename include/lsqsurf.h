@@ -183,6 +183,15 @@ int lsq_set_column_blocks_affine(lsq_handle* h, int64_t n_blocks, int32_t k, con
 int lsq_shape(lsq_handle* h, int64_t* m, int64_t* n, int64_t* nnz);
 /* Download the formed A (selected rows only, in row order; canonical CSR, sorted columns). */
 int lsq_get_csr(lsq_handle* h, int64_t* indptr, int32_t* indices, double* data);
+/* Full CSR of a lazily formed system.  lsq_set_matrix_stencil on one GPU stores only the data rows
+ * of G (the stencil rows live as part descriptors); these calls form the full G and Gᵀ on the
+ * device and keep them: lsq_get_csr, lsq_spmv / lsq_spmv_rows past the data rows, the dense
+ * (precond 2) and band (precond 5) factors, lsq_cov_band*, the mixed multigrid set-up, the
+ * assembled SELL operator (precond 0/1 LSQR without the stencil operator) and the distributed
+ * relabelling.  lsq_shape does not.  lsq_release_full_csr frees G / Gᵀ / the SELL copies again
+ * (the factors already built stay valid); *released = 0 when there was nothing to free (formed
+ * eagerly, never expanded, or relabelled for ranks). */
+int lsq_release_full_csr(lsq_handle* h, int32_t* released);
 
 /* ---- solve and products ----------------------------------------------------------------- */
 /* x = argmin || A x - diag(row_weight)·mask·b ||.  b has length m (unweighted rhs, all rows);

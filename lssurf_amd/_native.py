@@ -52,7 +52,7 @@ class LsqStats(ctypes.Structure):
 EXPORTS = ['lsq_default_opts', 'lsq_create', 'lsq_destroy', 'lsq_last_error', 'lsq_set_col_map',
            'lsq_set_matrix_coo', 'lsq_set_matrix_stencil', 'lsq_set_stencil_fields', 'lsq_set_row_weight',
            'lsq_set_row_mask',
-           'lsq_set_column_blocks', 'lsq_set_column_blocks_affine', 'lsq_shape', 'lsq_get_csr',
+           'lsq_set_column_blocks', 'lsq_set_column_blocks_affine', 'lsq_shape', 'lsq_get_csr', 'lsq_release_full_csr',
            'lsq_solve', 'lsq_spmv', 'lsq_spmv_rows', 'lsq_rows_sumsq', 'lsq_data_colsum', 'lsq_iterate', 'lsq_profile_kernels', 'lsq_cg_available', 'lsq_profile_cg', 'lsq_mg_info', 'lsq_mg_apply', 'lsq_normal_apply', 'lsq_sell_info', 'lsq_sigma_x', 'lsq_cov_band', 'lsq_cov_band_window', 'lsq_cov_band_windows', 'lsq_set_band_order', 'lsq_band_factor',
            'lsq_get_rinv', 'lsq_dist_unique_id', 'lsq_create_dist', 'lsq_dist_comm_info', 'lsq_dist_referenced_cols',
            'lsq_dist_set_layout', 'lsq_dist_set_halo', 'lsq_dist_set_global', 'lsq_vgroup_create', 'lsq_vgroup_rank', 'lsq_vgroup_solve', 'lsq_vgroup_iterate',
@@ -89,6 +89,7 @@ def load():
         'lsq_set_column_blocks_affine': ([P, i64, i32, P, P, P, P], ctypes.c_int),
         'lsq_shape': ([P, P, P, P], ctypes.c_int),
         'lsq_get_csr': ([P, P, P, P], ctypes.c_int),
+        'lsq_release_full_csr': ([P, P], ctypes.c_int),
         'lsq_solve': ([P, P, P, P, P], ctypes.c_int),
         'lsq_spmv': ([P, i32, P, P], ctypes.c_int),
         'lsq_spmv_rows': ([P, i64, i64, P, P], ctypes.c_int),

@@ -249,6 +249,15 @@ int lsq_shape(lsq_handle* h, int64_t* m, int64_t* n, int64_t* nnz) {
     });
 }
 
+int lsq_release_full_csr(lsq_handle* h, int32_t* released) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_release_full_csr: no matrix");
+        const bool r = lsq::release_full_csr(S);
+        if (released) *released = r ? 1 : 0;
+        return 0;
+    });
+}
+
 int lsq_get_csr(lsq_handle* h, int64_t* indptr, int32_t* indices, double* data) {
     return guarded(h, [&](lsq::System& S) {
         if (!S.G.rp.p) return fail(S, "lsq_get_csr: no matrix");

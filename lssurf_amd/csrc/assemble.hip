@@ -523,11 +523,23 @@ void ensure_full_csr(System& S) {
     graph_cache_drop(&S);   // G is reallocated (a captured batch may hold the data-row CSR's pointers)
     gen_rows_csr(S, S.gen_py.p, S.gen_px.p, S.gen_pt.n ? S.gen_pt.p : nullptr, S.G.m);
     S.g_full = true;
-    S.gen_py = DBuf<double>();
-    S.gen_px = DBuf<double>();
-    S.gen_pt = DBuf<double>();
-    S.gen_ctx.clear();
+    // the generation context stays (24 B per data row) so release_full_csr can drop G / GT again
     full_transpose(S);
+}
+
+bool release_full_csr(System& S) {
+    if (!S.g_full || S.gen_ctx.empty() || S.dist) return false;   // nothing formed lazily, or relabelled
+    graph_cache_drop(&S);
+    S.sell_built = false;
+    S.A = Sell();
+    S.AT = Sell();
+    S.GT = Csr{};
+    S.G = Csr{};
+    gen_rows_csr(S, S.gen_py.p, S.gen_px.p, S.gen_pt.n ? S.gen_pt.p : nullptr, S.mfh.npts);   // data rows only
+    S.g_full = false;
+    S.cs_mode = -1;   // the SELL values are gone; the next refresh fills the data rows' copies again
+    S.iter_ready = false;
+    return true;
 }
 
 int64_t stored_rows(const System& S) { return S.g_full ? S.G.m : S.mfh.npts; }

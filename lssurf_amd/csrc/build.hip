@@ -923,6 +923,7 @@ void referenced_cols(System& S, uint8_t* h_flags) {
 
 void relabel_columns(System& S, const int32_t* h_map, int64_t n_local) {
     ensure_full_csr(S);
+    S.gen_ctx.clear();   // G no longer regenerates from the formation (release_full_csr refuses)
     S.dmf.ok = 0;   // the matrix-free data rows address the formation's column space
     DBuf<int32_t> map(std::max<int64_t>(S.G.n, 1));
     map.upload(h_map, S.G.n, S.stream);

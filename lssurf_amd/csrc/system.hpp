@@ -513,6 +513,7 @@ void relabel_columns(System& S, const int32_t* h_map, int64_t n_local);
 
 // assemble.hip: the full G / GT of a lazily formed structured system (no-op when formed)
 void ensure_full_csr(System& S);
+bool release_full_csr(System& S);   // back to data rows only (false: not a lazily formed system)
 int64_t stored_rows(const System& S);            // rows of G whose entries are stored
 
 // build.hip

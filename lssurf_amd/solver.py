@@ -141,6 +141,13 @@ class LSQSolver:
         self._check(self._L.lsq_get_csr(self._h, ptr(rp), ptr(ci), ptr(v)), 'lsq_get_csr')
         return sp.csr_matrix((v[:z], ci[:z], rp), shape=(m, n))
 
+    def release_full_csr(self):
+        """Free the full G / Gᵀ (and SELL copies) that lsq_get_csr, the dense / band factors or
+        lsq_spmv formed on a lazily formed structured system; True when something was freed."""
+        r = ctypes.c_int32()
+        self._check(self._L.lsq_release_full_csr(self._h, ctypes.byref(r)), 'lsq_release_full_csr')
+        return bool(r.value)
+
     # ---- solve -------------------------------------------------------------------------------
     def solve(self, b, x0=None, atol=1e-10, btol=1e-10, conlim=1e8, maxit=0, precond=1, batch=0,
               use_graph=True, op=0, method=0, b_rows=0, anorm0=0.0):

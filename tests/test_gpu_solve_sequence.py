@@ -58,3 +58,34 @@ def test_mg_mg_bj_lsqr_sequence_with_reweighting(gpu_available):
             _check(x, xs, label)
     finally:
         fs.close()
+
+
+def test_release_full_csr_then_solve_again(gpu_available):
+    """ADVICE r4: the calls that form the full G / Gᵀ of a lazily formed system keep them;
+    lsq_release_full_csr drops them again.  Every solver still reaches the golden solution
+    afterwards (the band factor forms them once more), and shape() stays the same."""
+    g, fs, w, rhs = _golden_system('sf3d_eq_edit')
+    keep_all = np.ones(fs.n_data, bool)
+    try:
+        shape0 = fs.solver.shape()
+        assert not fs.solver.release_full_csr()            # formed lazily, never expanded
+        A = fs.solver.get_csr()                            # forms G / Gᵀ
+        assert A.shape == shape0[:2] and A.nnz == shape0[2]
+        for label, opts in (('band', dict(precond=5, method=0)),
+                            ('release', None),
+                            ('mg', dict(precond=4, method=1)),
+                            ('bj', dict(precond=3, method=1)),
+                            ('lsqr', dict(precond=3, method=0)),
+                            ('band again', dict(precond=5, method=0)),
+                            ('release again', None),
+                            ('mg last', dict(precond=4, method=1))):
+            if opts is None:
+                assert fs.solver.release_full_csr(), label
+                assert not fs.solver.release_full_csr(), label
+                assert fs.solver.shape() == shape0, label
+                continue
+            x = fs.solve(w, keep_all, rhs, **TOL, **opts)
+            _check(x, g['x'], label)
+        assert (fs.solver.get_csr() != A).nnz == 0
+    finally:
+        fs.close()
