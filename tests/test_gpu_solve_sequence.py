@@ -86,6 +86,8 @@ def test_release_full_csr_then_solve_again(gpu_available):
                 continue
             x = fs.solve(w, keep_all, rhs, **TOL, **opts)
             _check(x, g['x'], label)
-        assert (fs.solver.get_csr() != A).nnz == 0
+            if label == 'band':
+                Aw = fs.solver.get_csr()                   # with the solve's row weights
+        assert (fs.solver.get_csr() != Aw).nnz == 0
     finally:
         fs.close()
