@@ -467,6 +467,122 @@ __global__ __launch_bounds__(BLOCK) void k_band_sweep(BandDev b, int64_t j0, con
     }
 }
 
+// The identity sweeps (the diagonal of N⁻¹): NC of a tile's 64 right-hand sides per workgroup,
+// TB / NC workgroups per tile.  Wave v takes output rows 16v … 16v + 15 and all NC columns, with
+// two MFMA chains per 16-column tile (k parity).  Measured at 256²×12 with one lane (t256,
+// `gpurun_out/r5s`; the k_band_sweep layout before it took 10.6–10.8 s):
+//   NC = 64 (default)   10.3 s
+//   NC = 32             11.3 s
+//   NC = 16             14.9 s
+// Each chunk reads the R tiles again, and the sweeps are bound by the bytes they move.  PMC
+// (r5q2): every tile comes from beyond L2, 2.3 TB/s.  Neither a second pair of tiles in flight
+// nor two waves per SIMD moved the time (r5r, r5r2).
+template <int NC>
+__global__ __launch_bounds__(BLOCK) void k_band_sweep_id(BandDev b, int64_t j0, const int64_t* __restrict__ sp,
+                                                         double* __restrict__ ring, double* __restrict__ out) {
+    constexpr int NCH = TB / NC, LDB = NC + 1, NT = NC / 16;
+    constexpr int NA = (int)(TT / 2 / BLOCK), NBV = TB * NC / 2 / BLOCK;
+    __shared__ double A[TB * LDP];
+    __shared__ double B[TB * LDB];
+    __shared__ double red[4][4][NC];
+    const int64_t rt = blockIdx.x / NCH;
+    const int ch = (int)(blockIdx.x % NCH);
+    const int64_t K0 = sp ? sp[rt] : j0 + rt;
+    const int64_t W1 = b.w + 1, YT = (int64_t)TB * NC;   // a ring slot: 64 rows × NC columns
+    double* Rg = ring + (int64_t)blockIdx.x * W1 * YT;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, li = lane & 15, lk = lane >> 4;
+    const int r0 = wv * 16;
+    double2 ra[NA], rb[NBV];
+    auto load = [&](int64_t I, int64_t K) {
+        const double2* a2 = reinterpret_cast<const double2*>(btile(b.R, b.w, I, K));
+        const double2* b2 = reinterpret_cast<const double2*>(Rg + (I % W1) * YT);
+#pragma unroll
+        for (int i = 0; i < NA; ++i) ra[i] = a2[threadIdx.x + BLOCK * i];
+#pragma unroll
+        for (int i = 0; i < NBV; ++i) rb[i] = b2[threadIdx.x + BLOCK * i];
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const int idx = 2 * (threadIdx.x + BLOCK * i), r = idx >> 6, c = idx & 63;
+            A[r * LDP + c] = ra[i].x;
+            A[r * LDP + c + 1] = ra[i].y;
+        }
+#pragma unroll
+        for (int i = 0; i < NBV; ++i) {
+            const int idx = 2 * (threadIdx.x + BLOCK * i), r = idx / NC, c = idx % NC;
+            B[r * LDB + c] = rb[i].x;
+            B[r * LDB + c + 1] = rb[i].y;
+        }
+    };
+    // acc[t][par] += Aᵀ B over the wave's rows, 16-column tile t, k parity par
+    auto mma = [&](d4 (&acc)[NT][2]) {
+#pragma unroll 4
+        for (int k0 = 0; k0 < TB; k0 += 4) {
+            const int k = k0 + lk, par = (k0 >> 2) & 1;
+            const double a = A[k * LDP + r0 + li];
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+                acc[t][par] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, B[k * LDB + 16 * t + li], acc[t][par], 0, 0, 0);
+        }
+    };
+    auto zero = [&](d4 (&acc)[NT][2]) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t][0] = acc[t][1] = d4{0.0, 0.0, 0.0, 0.0};
+    };
+    double ss[NT] = {};
+    for (int64_t K = K0; K < b.T; ++K) {
+        d4 acc[NT][2];
+        zero(acc);
+        const int64_t I0 = max<int64_t>(K0, K - b.w);
+        if (I0 < K) load(I0, K);
+        for (int64_t I = I0; I < K; ++I) {
+            __syncthreads();
+            store();
+            __syncthreads();
+            if (I + 1 < K) load(I + 1, K);
+            mma(acc);
+        }
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < TT; idx += BLOCK) A[(idx >> 6) * LDP + (idx & 63)] = b.D[K * TT + idx];
+        for (int idx = threadIdx.x; idx < TB * NC; idx += BLOCK) {
+            const int r = idx / NC, c = idx % NC;
+            B[r * LDB + c] = (K == K0 && r == ch * NC + c) ? 1.0 : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) B[(r0 + lk + 4 * g) * LDB + 16 * t + li] -= acc[t][0][g] + acc[t][1][g];
+        __syncthreads();
+        zero(acc);
+        mma(acc);   // D_Kᵀ · X
+        double* Yk = Rg + (K % W1) * YT;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const double v = acc[t][0][g] + acc[t][1][g];
+                Yk[(r0 + lk + 4 * g) * NC + 16 * t + li] = v;
+                ss[t] += v * v;
+            }
+        __threadfence();
+        // the next step's first ring load (before its loop's barrier) may read this very slot
+        // (step K0 + 1 reads Y_K0): every thread's stores must have landed
+        __syncthreads();
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) red[wv][lk][16 * t + li] = ss[t];
+    __syncthreads();
+    if (threadIdx.x < NC) {
+        const int c = threadIdx.x;
+        double sum = 0.0;
+        for (int w = 0; w < 4; ++w)
+            for (int l = 0; l < 4; ++l) sum += red[w][l][c];
+        out[K0 * TB + ch * NC + c] = sum;
+    }
+}
+
 // E[perm[j]] = sqrt(ss_j)·s_j from the identity sweeps (perm null: E[j], window order)
 __global__ __launch_bounds__(BLOCK) void k_band_diag_sweep(int64_t n, const int32_t* __restrict__ perm,
                                                            const double* __restrict__ ssq,
@@ -775,15 +891,20 @@ __global__ __launch_bounds__(BLOCK) void k_band_pinv(int64_t n, const int32_t* _
     for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLOCK) pinv[perm[j]] = (int32_t)j;
 }
 
-// launch the sweeps of `nwg` workgroups in batches whose rings fit `ring` (cap workgroups each)
+// the identity sweeps' column chunk (k_band_sweep_id; -DBAND_NC=32/16 at build time, A/B)
+#ifndef BAND_NC
+#define BAND_NC 64
+#endif
+// launch the sweeps of `nwg` workgroups in batches whose rings fit `ring` (cap workgroups each;
+// the identity sweeps: cap tiles, each TB / BAND_NC workgroups of TB / BAND_NC of a tile's ring)
 template <bool IDENT>
 void run_sweeps(hipStream_t st, const BandDev& b, int64_t nwg, int64_t cap, const int64_t* sp, const int64_t* segK,
                 const int64_t* segE, const int32_t* el, const double* ev, const double* sc, double* ring, double* out) {
     for (int64_t g0 = 0; g0 < nwg; g0 += cap) {
         const int64_t g = std::min(cap, nwg - g0);
-        if (IDENT)   // sp: the tiles to sweep (null: tiles g0 … g0 + g − 1)
-            hipLaunchKernelGGL(k_band_sweep<true>, dim3((unsigned)g), dim3(BLOCK), 0, st, b, g0, sp ? sp + g0 : nullptr,
-                               segK, segE, el, ev, sc, ring, out);
+        if (IDENT)   // sp: the tiles to sweep (null: tiles g0 … g0 + g − 1), BAND_NC columns per workgroup
+            hipLaunchKernelGGL(k_band_sweep_id<BAND_NC>, dim3((unsigned)(g * (TB / BAND_NC))), dim3(BLOCK), 0, st, b, g0,
+                               sp ? sp + g0 : nullptr, ring, out);
         else
             hipLaunchKernelGGL(k_band_sweep<false>, dim3((unsigned)g), dim3(BLOCK), 0, st, b, (int64_t)0, sp + g0, segK,
                                segE, el, ev, sc, ring, out + g0 * TB);
