@@ -802,6 +802,7 @@ void graph_cache_drop(const System* S) {
             (void)hipGraphExecDestroy(c->exec);
             *c = GraphCache{};
         }
+    if (S && S->mg) mg_graph_drop(S->mg);
 }
 
 int lsqr_solve(System& S, const double* h_b, double* h_x, const lsq_opts& o, lsq_stats* stats) {

@@ -252,6 +252,7 @@ struct CgVar {
 };
 struct MgHier;   // multigrid hierarchy (mg.inc)
 void mg_free(MgHier* h);
+void mg_graph_drop(MgHier* h);   // its captured replicated-level V-cycle (ranks)
 struct CgDesc {
     int32_t n_grids, ntiles, lds_max, colmode;
     int32_t nedge, maxt3, pad[2];            // column mode: workgroups of the CG iteration's k_cg_xedge (pad[0]: <8>;
