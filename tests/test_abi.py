@@ -68,3 +68,14 @@ def test_device_group_fence_releases_ranks_on_failure():
     for fail in (0, 1, 3):
         assert L.lsq_fence_selftest(4, fail, 7) == 3
     assert L.lsq_fence_selftest(1, 0, 3) == 0
+
+
+def test_library_has_no_unresolved_symbols():
+    """Bound eagerly (RTLD_NOW), the library resolves every symbol it references — a function
+    declared in the library's own headers but defined with internal linkage (an anonymous
+    namespace) loads lazily here and fails only on the GPU box."""
+    from lssurf_amd import _native
+    if not os.path.exists(_native.LIB_PATH):
+        from lssurf_amd import build
+        build.build()
+    ctypes.CDLL(_native.LIB_PATH, mode=os.RTLD_NOW | os.RTLD_LOCAL)
