@@ -183,6 +183,15 @@ __device__ __forceinline__ float lf_val(lf_t v) {
     return __uint_as_float((uint32_t)v << 16);
 #endif
 }
+// Column j and row j of a packed block factor (M[r(r+1)/2 + c] = entry (r, c), r ≥ c) with one LDS
+// read per entry: fv[i] = (j, i) for i ≤ j, (i, j) for i > j, 0 past the block (k) or off a live
+// lane.  The two block products take fv[i] for i ≤ j and for i ≥ j (the diagonal in both).
+template <int K>
+__device__ __forceinline__ void lf_rowcol(const lf_t* M, int j, int k, bool mine, float (&fv)[K]) {
+    const int jj = j * (j + 1) / 2;
+#pragma unroll
+    for (int i = 0; i < K; ++i) fv[i] = (mine && i < k) ? lf_val(M[i <= j ? jj + i : i * (i + 1) / 2 + j]) : 0.0f;
+}
 __device__ __forceinline__ lf_t lf_round(double d) {
 #ifdef LSQ_LF_F32
     return (float)d;
