@@ -198,10 +198,15 @@ def iterate_fit(data, system, rhs, TCinv, G_data, Gc, in_TSE, timing, args, grid
     N_editable = np.sum(data.editable) if 'editable' in data.fields else data.size
     sigma_extra = np.zeros_like(data.z)
     last_iteration = args['max_iterations'] <= 1
-    m0 = np.zeros(system.n_full)
     x = None
     rs_data = None
     timing['lsq_iters'] = 0
+    # max |Δdz| between iterations (smooth_fit.py:180) on the compact solution: the dz columns are one
+    # contiguous run of the ascending keep_cols, and the removed ones are 0 in every m0.  The full
+    # m0 is expanded only where it is returned or read (no 10⁷-entry scatter per iteration at C4).
+    dsl = _as_slice(Gc.TOC['cols']['dz'])
+    kdz = tuple(int(k) for k in np.searchsorted(system.keep_cols, [dsl.start, dsl.stop])) \
+        if isinstance(dsl, slice) else None
     # row weights 1/sqrt(E_all²) with E_all = 1/TCinv (smooth_fit.py:103, 129): |TCinv| — the caller's
     # array itself when positive (no pass over, or copy of, the 77 M rows at C4).  sqrt(fl(x²)) = |x|
     # in IEEE arithmetic, so the reference's weight is 1/|fl(1/TCinv)|, which can differ from |TCinv|
@@ -220,7 +225,7 @@ def iterate_fit(data, system, rhs, TCinv, G_data, Gc, in_TSE, timing, args, grid
         if args['VERBOSE']:
             print('starting device lsqr solve for iteration %d at %s' % (iteration, ctime()), flush=True)
         tic = time()
-        m0_last = m0
+        x_last = x
         x0 = x if (args['lsq_warm_start'] and x is not None) else None
         dense_ok = getattr(system, 'dense_ok', True)
         mg = args['lsq_precond'] == 'auto' and (system.keep_cols.size > args['lsq_dense_max'] or not dense_ok) and \
@@ -251,7 +256,7 @@ def iterate_fit(data, system, rhs, TCinv, G_data, Gc, in_TSE, timing, args, grid
             print(f"smooth_fit: LSQR reached its iteration limit ({system.stats['iters']}) before the "
                   f"requested tolerance; raise lsq_maxit or use lsq_precond=2", flush=True)
         system.stats['precond'] = opts['precond']
-        m0 = system.expand(x)
+        system.last_x = x   # compact solution: z_est and the constraint statistics read it, not m0
         timing['sparseqr_solve'] = time() - tic
         timing['lsq_iters'] += int(system.stats['iters'])
         timing.setdefault('lsq_iters_per_solve', []).append(int(system.stats['iters']))
@@ -278,14 +283,19 @@ def iterate_fit(data, system, rhs, TCinv, G_data, Gc, in_TSE, timing, args, grid
         if 'editable' in data.fields:
             in_TSE[data.editable == 0] = in_TSE_original[data.editable == 0]
         if args['DEM_tol'] is not None:
-            in_TSE = check_data_against_DEM(in_TSE, data, m0, G_data, args['DEM_tol'])
+            in_TSE = check_data_against_DEM(in_TSE, data, system.expand(x), G_data, args['DEM_tol'])
         if not np.any(in_TSE):
             if args['VERBOSE']:
                 print('Edited data empty, returning')
-            return m0, sigma_extra, in_TSE, rs_data
-        dsl = _as_slice(Gc.TOC['cols']['dz'])
-        ddz = np.subtract(m0_last[dsl], m0[dsl])   # max |Δdz| (smooth_fit.py:180), one temporary
-        if np.max(np.abs(ddz, out=ddz)) < args['converge_tol_dz'] and iteration > args['min_iterations']:
+            return system.expand(x), sigma_extra, in_TSE, rs_data
+        if kdz is not None:
+            xs = x[kdz[0]:kdz[1]]
+            ddz = np.abs(xs) if x_last is None else np.subtract(x_last[kdz[0]:kdz[1]], xs)
+            dmax = float(np.max(np.abs(ddz, out=ddz))) if ddz.size else 0.0
+        else:
+            m_last = system.expand(x_last) if x_last is not None else np.zeros(system.n_full)
+            dmax = float(np.max(np.abs(m_last[dsl] - system.expand(x)[dsl])))
+        if dmax < args['converge_tol_dz'] and iteration > args['min_iterations']:
             if args['VERBOSE']:
                 print('Solution identical to previous iteration with tolerance %3.1f, exiting after iteration %d'
                       % (args['converge_tol_dz'], iteration))
@@ -314,7 +324,7 @@ def iterate_fit(data, system, rhs, TCinv, G_data, Gc, in_TSE, timing, args, grid
         if iteration == args['max_iterations'] - 2:
             last_iteration = True
         timing['edit'] = timing.get('edit', 0.) + time() - tic_edit
-    return m0, sigma_extra, in_TSE, rs_data
+    return (system.expand(x) if x is not None else np.zeros(system.n_full)), sigma_extra, in_TSE, rs_data
 
 
 def _toc_slice(op, name):
@@ -348,7 +358,10 @@ def _device_constraint_stats(system, m0, Gc, R, RMS):
             names.append(eq_type)
             ranges.append((system.n_data + rows.start, rows.stop - rows.start))
     if names:
-        sw, su = system.rows_sumsq(m0[system.keep_cols], ranges)
+        x = getattr(system, 'last_x', None)   # the compact solution m0 was expanded from (iterate_fit)
+        if x is None or x.size != np.size(system.keep_cols):
+            x = m0[system.keep_cols]
+        sw, su = system.rows_sumsq(x, ranges)
         for name, (first, count), a, b in zip(names, ranges, sw, su):
             R[name] = a
             RMS[name] = np.sqrt(b / count)
@@ -571,7 +584,9 @@ def smooth_fit(**kwargs):
             valid_data[valid_data] = in_TSE
             data.assign({'three_sigma_edit': in_TSE})
             data.assign({'sigma_extra': sigma_extra})
-            data.assign({'z_est': np.reshape(system.data_forward(m0[keep_cols]), data.shape)})
+            x_c = getattr(system, 'last_x', None)   # m0[keep_cols], without the 10⁷-entry gather
+            data.assign({'z_est': np.reshape(system.data_forward(x_c if x_c is not None else m0[keep_cols]),
+                                             data.shape)})
             if args['mask_update_function'] is not None:
                 averaging_ops = {}
                 parse_model(m, m0, data, R, RMS, G_data, averaging_ops, Gc, Ec(), grids, args)
