@@ -29,8 +29,12 @@ def main(cfg):
     stop.set()
     tim = {k: v for k, v in S['timing'].items() if not isinstance(v, dict) or k.startswith('E_')}
     sz = S['E']['sigma_z0'].sigma_z0
+    import hashlib
+    import numpy as np
+    digest = hashlib.sha256(np.ascontiguousarray(np.asarray(sz, dtype=np.float64)).tobytes()).hexdigest()[:16]
     print(json.dumps({'config': cfg, 'wall_s': wall, 'timing': tim,
                       'sigma_z0_median': float(sorted(sz.ravel())[sz.size // 2]),
+                      'sigma_z0_sha16': digest,   # bit-level identity of σ_z0 between builds / switches
                       'approximate': getattr(S['E']['sigma_z0'], 'approximate', None)}, default=float), flush=True)
 
 
