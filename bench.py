@@ -136,7 +136,40 @@ class _Dist:
         return d
 
 
-def cpu_baseline(fs, w, b_weighted, sample_iters, threads, method=0):
+def host_cores():
+    """The host cores this process may use ('all host cores, record nproc'):
+    nproc (os.cpu_count), the affinity mask, the cgroup CPU quota (cpu.max: a container's share
+    of a larger machine) and the socket count.  usable = min(affinity, ceil(quota))."""
+    import math
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    for path in ('/sys/fs/cgroup/cpu.max', '/sys/fs/cgroup/cpu/cpu.cfs_quota_us'):
+        try:
+            parts = open(path).read().split()
+        except OSError:
+            continue
+        if path.endswith('cpu.max') and parts and parts[0] != 'max':
+            quota = float(parts[0]) / float(parts[1] if len(parts) > 1 else 100000)
+        elif path.endswith('quota_us') and parts and int(parts[0]) > 0:
+            period = float(open('/sys/fs/cgroup/cpu/cpu.cfs_period_us').read().split()[0])
+            quota = float(parts[0]) / period
+        break
+    sockets = set()
+    for c in os.sched_getaffinity(0) if hasattr(os, 'sched_getaffinity') else range(nproc):
+        try:
+            sockets.add(open(f'/sys/devices/system/cpu/cpu{c}/topology/physical_package_id').read().strip())
+        except OSError:
+            pass
+    usable = aff if quota is None else max(1, min(aff, int(math.ceil(quota))))
+    return {'nproc': nproc, 'affinity': aff, 'cgroup_quota': quota, 'sockets': len(sockets) or None,
+            'usable': usable}
+
+
+def cpu_baseline(fs, w, b_weighted, sample_iters, threads, method=0, csr=True):
     """The same algorithm on this host's cores, on the same system and the same weighted rhs, a
     bounded sample of iterations: CGNR + block-Jacobi with the GPU solve's node blocks when the GPU
     line is CGNR — on the GPU's operator representation (oracle/cgnr_struct_cpu.c: stencil rows from
@@ -159,6 +192,8 @@ def cpu_baseline(fs, w, b_weighted, sample_iters, threads, method=0):
                                  f'{st["time_s"]:.1f} s after {st["setup_s"]:.1f} s of point sort and block factors'}
             except ValueError as e:   # interpolation grids on different lattices: the CSR kind only
                 log(f'bench: structured CPU baseline unavailable ({e})')
+        if out is not None and not csr:
+            return out
         A = fs.solver.get_csr()
         x, st = cpu.cgnr_bj(A, b_weighted, *fs.blocks, fixed_iters=sample_iters, threads=threads)
         csr = {'value': st['iters'] / st['time_s'], 'unit': 'CGNR iters/s', 'cores': int(st['threads']),
@@ -440,8 +475,20 @@ def main():
             r['solve_comm_bytes_per_iter'] = b
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not args.dist:
-        threads = min(os.cpu_count() or 1, 16)
+        hc = host_cores()
+        threads = hc['usable']   # every core this process may use, one OpenMP thread per core, pinned
+        os.environ.setdefault('OMP_PROC_BIND', 'close')   # read by libgomp when oracle/_cpu.so loads
+        os.environ.setdefault('OMP_PLACES', 'cores')
         cpu = cpu_baseline(fs, w, w * rhs, args.cpu_iters, threads, meth)
+        cpu['host'] = hc
+        if threads != 16 and os.environ.get('LSQ_BENCH_CPU16', '1') != '0' and meth == 1 \
+                and getattr(fs, 'desc', None) is not None:
+            # rounds 4-5 reported 16 threads: kept beside the all-cores figure for continuity
+            try:
+                c16 = cpu_baseline(fs, w, w * rhs, args.cpu_iters, 16, meth, csr=False)
+                cpu['threads16'] = {k: c16[k] for k in ('value', 'unit', 'cores')}
+            except Exception as e:   # noqa: BLE001 - reporting only
+                log(f'bench: 16-thread CPU baseline failed ({e})')
         if args.cpu_solve and solve:   # the CPU oracle to the same stopping rule, on the same A, b
             from oracle import cpu as ocpu
             xc, stc = ocpu.lsqr(fs.solver.get_csr(), w * rhs, atol=1e-10, btol=1e-10, conlim=1e8,

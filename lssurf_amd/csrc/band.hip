@@ -1310,16 +1310,24 @@ void band_cov_windows(System& S, int64_t nwin, const int64_t* win_ptr, const int
             const int64_t nsw = (int64_t)tiles.size(), nopw = nops > 0 ? (int64_t)so.sp.size() - 1 : 0;
             for (int64_t J : tiles) products += (T - J) * (int64_t)std::min<int64_t>(bw + 1, T - J);
             products += so.gemms;
-            const int64_t cap = std::max<int64_t>({nsw, nopw, 1});
-            const int64_t need = (band_tiles + T + cap * (bw + 1)) * TT * (int64_t)sizeof(double);
-            if (L.R.n < band_tiles * TT || L.ring.n < cap * (bw + 1) * TT) {
+            // sweep rings for up to `cap` concurrent workgroups (run_sweeps batches the rest): every
+            // tile of the interior at once when the device has the room, else as many as fit the
+            // free memory (band_cov's rule) — a wide band then sweeps in batches instead of failing
+            const int64_t want = std::max<int64_t>({nsw, nopw, 1}), ring_wg = (int64_t)(bw + 1) * TT;
+            int64_t cap = want;
+            if (L.R.n < band_tiles * TT || L.D.n < T * TT || L.ring.n < want * ring_wg) {
                 size_t free_b = 0, total_b = 0;
                 HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-                if ((double)need > 0.8 * (double)free_b)
+                const double grow_rd = (double)(std::max<int64_t>(band_tiles * TT - L.R.n, 0) +
+                                                std::max<int64_t>(T * TT - L.D.n, 0)) * sizeof(double);
+                const double room = 0.8 * (double)free_b + (double)L.ring.n * sizeof(double) - grow_rd;
+                cap = std::min<int64_t>(want, (int64_t)(room / ((double)ring_wg * sizeof(double))));
+                if (cap < 1)
                     throw Refused("lsq_cov_band_windows: a window band of " + std::to_string(bw) +
-                                  " tiles and its sweeps need " + std::to_string(need >> 20) +
-                                  " MiB, more than the device has free (fewer lanes: LSQ_E_LANES)");
+                                  " tiles needs " + std::to_string((int64_t)grow_rd >> 20) +
+                                  " MiB more, more than the device has free (fewer lanes: LSQ_E_LANES)");
             }
+            const int64_t need = (band_tiles + T + cap * (bw + 1)) * TT * (int64_t)sizeof(double);
             grow(L.R, band_tiles * TT);
             grow(L.D, T * TT);
             grow(L.sc, npad);

@@ -125,49 +125,57 @@ def window_cov(solver, grids, keep_cols, op=None, tile=WINDOW_TILE, margin=WINDO
         return a + np.flatnonzero(m)
 
     # every window (tile ± margin, the op rows of the tile's centre; op rows wider than that get a
-    # window of their own; last, the self-check: the most central tile with twice the margin), then
-    # the device runs them in chunks, several windows at a time (lsq_cov_band_windows)
-    wins = []   # (positions, inner flags or None, op rows or None)
-    for ty in range(0, ny, tile):
-        for tx in range(0, nx, tile):
-            pos = window(ty - margin, ty + tile + margin, tx - margin, tx + tile + margin)
-            yi, xi = iy_o[pos], ix_o[pos]
-            inner = (yi >= ty) & (yi < ty + tile) & (xi >= tx) & (xi < tx + tile)
-            rows = None if op is None else np.flatnonzero((oty == ty // tile) & (otx == tx // tile) & ~own)
-            wins.append((pos, inner, rows))
-    ntiles = len(wins)
+    # window of their own; last, the self-check: the most central tile with twice the margin) as a
+    # small spec; its positions are formed only when its batch goes to the device
+    # (lsq_cov_band_windows), so host memory stays O(WINDOW_BATCH windows) whatever the grid
+    def tile_win(ty, tx, mg):
+        pos = window(ty - mg, ty + tile + mg, tx - mg, tx + tile + mg)
+        yi, xi = iy_o[pos], ix_o[pos]
+        return pos, (yi >= ty) & (yi < ty + tile) & (xi >= tx) & (xi < tx + tile)
+
+    specs = [('tile', ty, tx) for ty in range(0, ny, tile) for tx in range(0, nx, tile)]
+    ntiles = len(specs)
     if op is not None and own.any():   # one window per distinct support box
         boxes = np.stack([y_lo, y_hi, x_lo, x_hi], axis=1)
         for b in np.unique(boxes[own], axis=0):
-            rows = np.flatnonzero(own & np.all(boxes == b, axis=1))
-            wins.append((window(b[0] - margin, b[1] + margin + 1, b[2] - margin, b[3] + margin + 1),
-                         None, rows))
-    nown = len(wins) - ntiles
+            specs.append(('own', b, np.flatnonzero(own & np.all(boxes == b, axis=1))))
+    nown = len(specs) - ntiles
     cy, cx = (ny // 2) // tile * tile, (nx // 2) // tile * tile
     m2 = 2 * margin
-    pos2 = window(cy - m2, cy + tile + m2, cx - m2, cx + tile + m2)
-    yi, xi = iy_o[pos2], ix_o[pos2]
-    inner2 = (yi >= cy) & (yi < cy + tile) & (xi >= cx) & (xi < cx + tile)
-    wins.append((pos2, inner2, None))
-    E2 = None
+    specs.append(('check', cy, cx))
+
+    def materialize(spec):   # (positions, inner flags or None, op rows or None)
+        if spec[0] == 'tile':
+            ty, tx = spec[1], spec[2]
+            pos, inner = tile_win(ty, tx, margin)
+            rows = None if op is None else np.flatnonzero((oty == ty // tile) & (otx == tx // tile) & ~own)
+            return pos, inner, rows
+        if spec[0] == 'own':
+            b = spec[1]
+            return window(b[0] - margin, b[1] + margin + 1, b[2] - margin, b[3] + margin + 1), None, spec[2]
+        pos, inner = tile_win(spec[1], spec[2], m2)
+        return pos, inner, None
+
+    E2 = pos2 = inner2 = None
     wmax = products = 0
     t_all = time()
-    batch = int(os.environ.get('LSQ_E_BATCH', WINDOW_BATCH))
-    for c0 in range(0, len(wins), max(batch, 1)):
-        chunk = wins[c0:c0 + max(batch, 1)]
+    batch = max(int(os.environ.get('LSQ_E_BATCH', WINDOW_BATCH)), 1)
+    for c0 in range(0, len(specs), batch):
+        chunk = [materialize(sp_) for sp_ in specs[c0:c0 + batch]]
         req = [(order[pos], inner if inner is not None else np.zeros(pos.size, bool),
                 op[rows] if (op is not None and rows is not None and rows.size) else None)
                for pos, inner, rows in chunk]
         Es, oes, info = solver.cov_band_windows(req)
         wmax, products = max(wmax, int(info[0])), products + int(info[3])
         for k, ((pos, inner, rows), (cols, _, _), Et, oe) in enumerate(zip(chunk, req, Es, oes)):
-            if c0 + k == len(wins) - 1:       # the self-check window
-                E2 = Et
+            if c0 + k == len(specs) - 1:       # the self-check window
+                E2, pos2, inner2 = Et, pos, inner
                 continue
             if inner is not None:
                 E[cols[inner]] = Et[inner]
             if oe is not None:
                 op_err[rows] = oe
+        del chunk, req, Es, oes
     # self-check: σ of the central tile's columns moves by the correlations the margin cut off
     # (conditional vs marginal variance)
     c2 = order[pos2][inner2]

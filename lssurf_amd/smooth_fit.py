@@ -190,6 +190,19 @@ def _solve_opts(args, n, has_blocks=False, multigrid=False, dense_ok=True):
                 method=meth)
 
 
+def _anorm_seed_ok(precond, weight, in_TSE, prev):
+    """May this CGNR solve seed its ‖A M^-1/2‖ estimate with the previous solve's (lsq_opts.anorm0)?
+    Column scaling and node-block M: always (the preconditioned Frobenius norm is sqrt(n) whatever
+    the weights and mask).  Multigrid: only with the previous solve's row weights (not after the
+    sigma_extra_relax re-weighting) and at most 1 % of the data rows re-masked by the edits."""
+    if precond in (1, 3):
+        return True
+    if prev is None or prev[0] is not weight or prev[1] is None:
+        return False
+    m = np.asarray(in_TSE, bool)
+    return m.shape == prev[1].shape and int(np.count_nonzero(m != prev[1])) <= 0.01 * max(m.size, 1)
+
+
 def iterate_fit(data, system, rhs, TCinv, G_data, Gc, in_TSE, timing, args, grids, sigma_extra_masks=None):
     """Outer editing loop (smooth_fit.py:100-210) around the device solve.  TCinv: the diagonal of
     the reference's TCinv (1/σ per row of [G_data; Gc])."""
@@ -214,6 +227,7 @@ def iterate_fit(data, system, rhs, TCinv, G_data, Gc, in_TSE, timing, args, grid
     # weights are a read-only view: nothing may edit them in place, since they alias TCinv.
     weight0 = (TCinv if TCinv.min() > 0 else np.abs(TCinv)).view()
     weight0.flags.writeable = False
+    prev_solve = None   # (row weights, data-row mask) of the previous solve: _anorm_seed_ok
     for iteration in range(args['max_iterations']):
         weight = weight0
         if last_iteration and args['sigma_extra_relax']:
@@ -235,10 +249,13 @@ def iterate_fit(data, system, rhs, TCinv, G_data, Gc, in_TSE, timing, args, grid
         opts = _solve_opts(args, system.keep_cols.size, system.has_blocks, mg, dense_ok)
         last = system.stats
         if args['lsq_reuse_anorm'] and last is not None and last.get('method') == 1 and \
-                opts['method'] == 1 and last.get('precond') == opts['precond']:
+                opts['method'] == 1 and last.get('precond') == opts['precond'] and \
+                _anorm_seed_ok(opts['precond'], weight, in_TSE, prev_solve):
             # the CGNR stopping rule starts from the previous solve's ‖A M^-1/2‖ estimate (lsq_opts
-            # .anorm0) instead of rebuilding it from zero: with node-block M the preconditioned
-            # Frobenius norm is sqrt(n) whatever the weights, so the estimate stays below it
+            # .anorm0) instead of rebuilding it from zero: with node-block M (or column scaling) the
+            # preconditioned Frobenius norm is sqrt(n) whatever the weights, so the estimate stays
+            # below it.  The multigrid M has no such invariant: there the seed is taken only when
+            # the weights are the previous solve's and at most 1 % of the data rows changed mask
             opts['anorm0'] = float(last['anorm'])
         try:
             x = system.solve(weight, in_TSE, rhs, x0=x0, **opts)
@@ -256,6 +273,7 @@ def iterate_fit(data, system, rhs, TCinv, G_data, Gc, in_TSE, timing, args, grid
             print(f"smooth_fit: LSQR reached its iteration limit ({system.stats['iters']}) before the "
                   f"requested tolerance; raise lsq_maxit or use lsq_precond=2", flush=True)
         system.stats['precond'] = opts['precond']
+        prev_solve = (weight, np.asarray(in_TSE, bool).copy() if opts['precond'] == 4 else None)
         system.last_x = x   # compact solution: z_est and the constraint statistics read it, not m0
         timing['sparseqr_solve'] = time() - tic
         timing['lsq_iters'] += int(system.stats['iters'])
@@ -484,8 +502,6 @@ def smooth_fit(**kwargs):
             raise NotImplementedError(f'smooth_fit: {key!r} is outside lssurf_amd (SURVEY.md §2)')
     if args.get('data_slope_sensors') is not None and len(args['data_slope_sensors']) > 0:
         raise NotImplementedError("smooth_fit: 'data_slope_sensors' is outside lssurf_amd")
-    if args.get('sigma_extra_keys') is not None:
-        raise NotImplementedError("smooth_fit: 'sigma_extra_keys' is outside lssurf_amd")
 
     valid_data = np.isfinite(args['data'].z)
     if 'sensor' not in args['data'].fields:
@@ -503,7 +519,16 @@ def smooth_fit(**kwargs):
                 'RMS': {}, 'timing': timing, 'E_RMS': args['E_RMS']}
     data = args['data'].copy_subset(valid_data)
     validate_by_dz_mask(data, grids, valid_data)
-    if args['sigma_extra_masks'] is not None:
+    if args['sigma_extra_keys'] is not None:
+        # one sigma_extra group per key: the data whose field takes any of the listed values
+        # (smooth_fit.py:442-447; the masks are over the valid subset already)
+        args['sigma_extra_masks'] = {}
+        for key, field_vals in args['sigma_extra_keys'].items():
+            mask = np.zeros_like(data.sensor, dtype=bool)
+            for field, vals in field_vals.items():
+                mask |= np.isin(getattr(data, field), vals)
+            args['sigma_extra_masks'][key] = mask
+    elif args['sigma_extra_masks'] is not None:
         for key in args['sigma_extra_masks']:
             args['sigma_extra_masks'][key] = args['sigma_extra_masks'][key][valid_data == 1]
     if data.size == 0:

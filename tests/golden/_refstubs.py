@@ -22,6 +22,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 REF = '/root/reference'
 CALLS = []          # (A_coo, b) recorded for every sparseqr.solve call
 RZ_CALLS = []       # A recorded for every sparseqr.rz call (compute_E)
+SOLS = []           # the exact solution returned by every sparseqr.solve call
 
 
 def sp_csr(A):
@@ -131,7 +132,9 @@ def install():
 
     def solve(A, b, tolerance=None):
         CALLS.append((A.tocsr().copy(), np.array(b, dtype=float).copy()))
-        return dense.ls_solve_dense(A, b)
+        x = dense.ls_solve_dense(A, b)
+        SOLS.append(x.copy())
+        return x
     sq.solve = solve
 
     def rz(A, b):

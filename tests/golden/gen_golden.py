@@ -20,6 +20,8 @@ tri.npz        I/O of the reference Cython kernels inv_tr_upper / propagate_qz_e
                spsolve_tr_upper on random upper-triangular CSR matrices (incl. overflow)
 sys_avg.npz    averaging products (avg_scales, z0_average_scale, avg_masks) and their errors
 kat.npz        the analytic amplitude KAT of notebooks/smooth_fit_demo.ipynb cell 8
+sys_sekeys.npz sigma_extra_keys: per-group sigma_extra from a data field (smooth_fit.py:442-447)
+sys_deep{1,3}.npz a 48²×12 system (27 648 unknowns) deep enough for the multigrid default, lean
 sys_aniso*.npz notebooks/smooth_fit_demo_aniso.ipynb's directional-smoothing systems (the notebook's
                own cells 8-10 and 15 executed from the notebook file on the reference LSsurf): the
                2-D notebook system at 41² / 37² and the C5 z0 + dz system at toy size
@@ -97,23 +99,31 @@ def synth_points(rng, W, ctr, n, with_t=True, outside=0):
     return x, y, t, z
 
 
-def run_sf(LS, stubs, name, data_dict, sf_kwargs, n_outliers=0, rng=None, extra=None):
+def run_sf(LS, stubs, name, data_dict, sf_kwargs, n_outliers=0, rng=None, extra=None, lean=False):
+    """lean: store no matrices (the inputs, the exact first solution x* the oracle returned to
+    the reference, and the outputs) — the fixtures of systems too large to commit their A."""
     import pointCollection as pc
     data = pc.data().from_dict(data_dict)
     stubs.CALLS.clear()
+    stubs.SOLS.clear()
     S = LS.smooth_fit(data=data, **sf_kwargs)
     out = {'in_' + k: np.asarray(v) for k, v in data_dict.items()}
     A, b = stubs.CALLS[0]
-    out.update(_csr_arrays('A', A))
-    out['b'] = b
     from oracle import dense
-    x = dense.ls_solve_dense(A, b)
-    out['x'] = x
-    out['x_opt'] = np.array(dense.optimality(A, b, x))
-    # last solve (after editing) as well
-    A2, b2 = stubs.CALLS[-1]
-    out.update(_csr_arrays('Alast', A2))
-    out['blast'] = b2
+    if lean:
+        out['x'] = stubs.SOLS[0]
+        out['x_opt'] = np.array(dense.optimality(A, b, stubs.SOLS[0]))
+        out['x_shape'] = np.array(A.shape)
+    else:
+        out.update(_csr_arrays('A', A))
+        out['b'] = b
+        x = dense.ls_solve_dense(A, b)
+        out['x'] = x
+        out['x_opt'] = np.array(dense.optimality(A, b, x))
+        # last solve (after editing) as well
+        A2, b2 = stubs.CALLS[-1]
+        out.update(_csr_arrays('Alast', A2))
+        out['blast'] = b2
     out['n_solves'] = np.array(len(stubs.CALLS))
     m = S['m']
     out['z0'] = m['z0'].z0
@@ -144,6 +154,9 @@ def run_sf(LS, stubs, name, data_dict, sf_kwargs, n_outliers=0, rng=None, extra=
     for k, v in S['E'].items():
         out['E_' + k] = np.asarray(getattr(v, k))
     out['kwargs'] = np.array(repr({k: v for k, v in sf_kwargs.items() if k != 'avg_masks'}))
+    if lean:   # the solution-derived grids other fixtures already pin: kept out of the lean file
+        out = {k: v for k, v in out.items() if not (k == 'm_all' or k.startswith('m_dzdt') or
+                                                      k.startswith('z0_') or k.startswith('dz_'))}
     for k, v in (extra or {}).items():
         out['in_' + k] = np.asarray(v)
     np.savez_compressed(os.path.join(HERE, f'sys_{name}.npz'), **out)
@@ -217,6 +230,45 @@ def gen_tide(LS, stubs):
     run_sf(LS, stubs, 'tide', {'x': x, 'y': y, 'time': t, 'z': z, 'sigma': np.full(x.size, 0.1), 'tide': tide},
            dict(W=W, ctr=ctr, spacing={'z0': 100., 'dz': 100., 'dt': 0.25}, E_RMS=E_RMS_NB,
                 reference_epoch=2, max_iterations=3, VERBOSE=False, dzdt_lags=[1], sigma_extra_relax=True))
+
+
+def gen_sekeys(LS, stubs):
+    """sigma_extra_keys (smooth_fit.py:442-447): two sigma_extra groups built from a data field
+    ('sensor' values {0, 1} and {2, 3}, the groups with different extra noise), outliers and 4
+    outer iterations, so calc_sigma_extra's per-group RDE (calc_sigma_extra.py:13-44) drives the
+    edits."""
+    rng = np.random.default_rng(20251125)
+    W = {'x': 1400., 'y': 1200., 't': 1.25}
+    ctr = {'x': 0., 'y': 0., 't': 0.}
+    x, y, t, z = synth_points(rng, W, ctr, 1000)
+    sensor = rng.integers(0, 4, x.size).astype(float)
+    z = z + np.where(sensor >= 2, rng.normal(0, 0.6, x.size), rng.normal(0, 0.05, x.size))
+    bad = rng.random(x.size) > 0.93
+    z[bad] += (rng.random(bad.sum()) - 0.5) * 40
+    run_sf(LS, stubs, 'sekeys', {'x': x, 'y': y, 'time': t, 'z': z, 'sigma': np.full(x.size, 0.1),
+                                 'sensor': sensor},
+           dict(W=W, ctr=ctr, spacing={'z0': 100., 'dz': 100., 'dt': 0.25}, E_RMS=E_RMS_NB,
+                reference_epoch=2, max_iterations=4, VERBOSE=False, dzdt_lags=[1],
+                sigma_extra_keys={'low': {'sensor': [0., 1.]}, 'high': {'sensor': [2., 3.]}}))
+
+
+def gen_deep(LS, stubs):
+    """A system deep enough for smooth_fit's default multigrid solver to run a real hierarchy
+    (VERDICT r5 #3a): 48 × 48 (y, x) nodes × 12 epochs, z0 and dz on one 100 m lattice,
+    2 points per (y, x) node (C4's density), n = 27 648 unknowns (above lsq_dense_max, so the
+    default is CGNR + the V-cycle: 48 → 25 → 13 → 7 → 4 nodes per side).  Run by the reference
+    with the exact dense oracle at max_iterations 1 and 3 (outliers: the 3-iteration run edits).
+    Lean fixtures: the inputs, the exact first solution and the outputs, no matrices."""
+    rng = np.random.default_rng(20251126)
+    W = {'x': 4700., 'y': 4700., 't': 2.75}
+    ctr = {'x': 0., 'y': 0., 't': 0.}
+    x, y, t, z = synth_points(rng, W, ctr, 2 * 48 * 48)
+    bad = rng.random(x.size) > 0.95
+    z[bad] += (rng.random(bad.sum()) - 0.5) * 40
+    for iters in (1, 3):
+        run_sf(LS, stubs, f'deep{iters}', {'x': x, 'y': y, 'time': t, 'z': z, 'sigma': np.full(x.size, 0.1)},
+               dict(W=W, ctr=ctr, spacing={'z0': 100., 'dz': 100., 'dt': 0.25}, E_RMS=E_RMS_NB,
+                    reference_epoch=5, max_iterations=iters, VERBOSE=False, dzdt_lags=[1]), lean=True)
 
 
 def gen_avg(LS, stubs):
@@ -477,7 +529,8 @@ def main():
     gens = {'stencils': lambda: gen_stencils(LS), 'tri': lambda: gen_tri(LS), 'lin2d': lambda: gen_lin2d(LS),
             'systems': lambda: gen_systems(LS, _refstubs), 'avg': lambda: gen_avg(LS, _refstubs),
             'kat': lambda: gen_kat(LS), 'aniso': lambda: gen_aniso(LS, _refstubs),
-            'eq_edit': lambda: gen_eq_edit(LS, _refstubs), 'tide': lambda: gen_tide(LS, _refstubs)}
+            'eq_edit': lambda: gen_eq_edit(LS, _refstubs), 'tide': lambda: gen_tide(LS, _refstubs),
+            'sekeys': lambda: gen_sekeys(LS, _refstubs), 'deep': lambda: gen_deep(LS, _refstubs)}
     for name in (sys.argv[1:] or list(gens)):   # e.g. `gen_golden.py aniso`: only those fixtures
         gens[name]()
 

@@ -1,4 +1,5 @@
-"""Parity at the BASELINE sizes (C4: 1024²×12 grid, 2 M points, 12.6 M unknowns; C5: 2048²×12, 8 M points)
+"""Parity at the BASELINE sizes (C2: 2-D 1024², 500 k points; C3: 512²×12, 1 M points; C4: 1024²×12
+grid, 2 M points, 12.6 M unknowns; C5: 2048²×12, 8 M points)
 through size-independent properties — the oracle cannot run here, so each property is one the
 exact answer must have:
   * the fused normal operator equals Gᵀ(w²∘(G p)) formed through the explicitly assembled CSR
@@ -132,3 +133,67 @@ def test_c5a_normal_operator_and_solvers(gpu_available, c5a):
         ratio = np.linalg.norm(fs.solver.spmv(w * r, trans=True)) / (anorm * np.linalg.norm(r))
         assert ratio <= 1e-7, (name, ratio)
     assert np.linalg.norm(xs['bj'] - xs['mg']) <= 1e-7 * np.linalg.norm(xs['mg'])
+
+
+def _build(config):
+    """FitSystem of BASELINE config c2 (2-D z0-only lin_op system) or c3 (smooth_fit 512²×12),
+    as bench.py forms it (first-iteration row weights, every row kept)."""
+    from lssurf_amd import synthetic
+    from lssurf_amd.smooth_fit import FitSystem
+    if config in synthetic.CONFIGS_2D:
+        G, Gc, grid, w, rhs = synthetic.system2d(config)
+        fs = FitSystem(G, Gc, np.arange(G.col_N), G.col_N, grids={'z0': grid})
+    else:
+        import lssurf_amd as LS
+        from lssurf_amd.constraint_functions import reference_epoch_keep_cols
+        D, kw = synthetic.points(config)
+        S = LS.smooth_fit(data=D, return_fit_objects=True, VERBOSE=False, **kw)
+        keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch'])
+        fs = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, grids=S['grids'])
+        w = 1. / np.concatenate((S['Ed'], S['Ec']))
+        rhs = np.zeros(w.size)
+        rhs[:S['data'].size] = S['data'].z
+    fs.solver.set_row_weight(w)
+    fs.solver.set_row_mask(np.ones(w.size, bool))
+    return fs, w, rhs
+
+
+@pytest.mark.parametrize('config', ['c2', 'c3'])
+def test_c2_c3_operator_and_solvers(gpu_available, config):
+    """BASELINE C2 and C3 at full size: the normal operator against the assembled CSR (≤ 1e-12)
+    and symmetric; every solver smooth_fit / bench.py would use on the system (multigrid where it
+    runs, block-Jacobi where there are node blocks, else column scaling; CGNR and LSQR) reaching a
+    solution that satisfies the normal equations (≤ 1e-7), the solutions agreeing (≤ 1e-7)."""
+    fs, w, rhs = _build(config)
+    try:
+        rng = np.random.default_rng(59)
+        u = np.zeros(fs.n_full)
+        v = np.zeros(fs.n_full)
+        u[fs.keep_cols] = rng.standard_normal(fs.keep_cols.size)
+        v[fs.keep_cols] = rng.standard_normal(fs.keep_cols.size)
+        qu, qv = fs.solver.normal_apply(u), fs.solver.normal_apply(v)
+        ref = _normal_ref(fs, w, u[fs.keep_cols])
+        assert np.linalg.norm(qu[fs.keep_cols] - ref) <= 1e-12 * np.linalg.norm(ref)
+        a, b_ = v @ qu, u @ qv
+        assert abs(a - b_) <= 1e-12 * (abs(a) + abs(b_))
+        anorm = _anorm2(fs)
+        b = w * rhs
+        pc = 3 if fs.has_blocks else 1
+        runs = [('cg', dict(precond=pc, method=1)), ('lsqr', dict(precond=pc, method=0))]
+        if fs.solver.cg_available(4)[0]:
+            runs.insert(0, ('mg', dict(precond=4, method=1)))
+        xs = {}
+        for name, opts in runs:
+            x, st = fs.solver.solve(rhs, atol=1e-10, btol=1e-10, conlim=1e8, b_rows=fs.n_data, **opts)
+            assert st['istop'] in (1, 2), (config, name, st)
+            xs[name] = x
+            r = b - w * fs.solver.spmv(x)
+            ratio = np.linalg.norm(fs.solver.spmv(w * r, trans=True)) / (anorm * np.linalg.norm(r))
+            assert ratio <= 1e-7, (config, name, ratio)
+        x0 = xs[runs[0][0]]
+        for name in xs:
+            assert np.linalg.norm(xs[name] - x0) <= 1e-7 * np.linalg.norm(x0), (config, name)
+        if config == 'c3':
+            assert 'mg' in xs   # the smooth_fit default at this size
+    finally:
+        fs.close()
