@@ -272,6 +272,20 @@ int lsq_cov_band_windows(lsq_handle* h, int64_t n_windows, const int64_t* win_pt
                          const uint8_t* inner, double* E, const int64_t* win_ops, const int64_t* op_ptr,
                          const int32_t* op_pos, const double* op_val, double* op_err, int64_t* info);
 
+/* Many windows with their bottom margin eliminated first (compute_E at scale; DESIGN.md §Error
+ * propagation, round 6): window w's columns are perm[win_ptr[w] .. win_ptr[w+1]) = A = [top margin
+ * rows, interior rows] in ascending band order, its last nib[w] columns being Ib (the interior rows
+ * the bottom margin's rows reach); bot_perm[bot_ptr[w] .. bot_ptr[w+1]) = B' = the band order of
+ * [Ib, bottom margin] REVERSED (bot_ptr[w+1] = bot_ptr[w]: no bottom margin).  B' is factored, its
+ * trailing Ib block gives the bottom margin's Schur complement onto Ib, which replaces A's (Ib, Ib)
+ * block; A is then factored and swept over the tiles holding an inner position, so the sweeps end
+ * at the interior.  E (window order, A's positions) equals lsq_cov_band_windows' E of the whole
+ * window [A, bottom margin] to rounding.  Fails (-3, "a deeper Ib is needed") when a row holds a
+ * column of A outside Ib and one of the bottom margin.  info as lsq_cov_band_windows. */
+int lsq_cov_band_windows_schur(lsq_handle* h, int64_t n_windows, const int64_t* win_ptr, const int32_t* perm,
+                               const uint8_t* inner, double* E, const int64_t* bot_ptr, const int32_t* bot_perm,
+                               const int64_t* nib, int64_t* info);
+
 /* The banded factor itself (replaces sparseqr.rz's R and E, smooth_fit.py:218 / the aniso notebook):
  * for the current weighted, masked A and the column order perm (nullable = natural),
  * (A·P)ᵀ(A·P) = RᵀR with R = R̃·S⁻¹, R̃ the upper band factor of the equilibrated S·Pᵀ(AᵀA)P·S.
@@ -390,7 +404,8 @@ int lsq_profile_kernels(lsq_handle* h, int32_t reps, int32_t op, double* out8);
 int lsq_cg_available(lsq_handle* h, int32_t precond);
 int lsq_profile_cg(lsq_handle* h, int32_t reps, int32_t precond, double* out8);
 /* Multigrid (precond 4) test hooks.  lsq_mg_info: out[0] = levels L, then per level
- * (S0, S1, n_full, removed epoch) — cap must hold 1 + 4L values.  lsq_mg_apply on level l's full
+ * (S0, S1, n_full, removed epoch) — cap must hold 1 + 4L values; with room for 2 + 4L, out[1 + 4L] =
+ * the first level of the one-workgroup tail V-cycle (k_mg_tail), −1 for none.  lsq_mg_apply on level l's full
  * column space (z0 grid then dz grid, in the system's order): what 0: y = N_l x (level 0: AᵀA;
  * coarse levels: Galerkin PᵀNP of the stencil rows + the (y, x)-lumped data rows), 1: y = the
  * V-cycle applied to x (level 0), 2: y[0] = the smoother's λ_max(M⁻¹N) estimate of level l.

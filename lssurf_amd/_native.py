@@ -53,7 +53,7 @@ EXPORTS = ['lsq_default_opts', 'lsq_create', 'lsq_destroy', 'lsq_last_error', 'l
            'lsq_set_matrix_coo', 'lsq_set_matrix_stencil', 'lsq_set_stencil_fields', 'lsq_set_row_weight',
            'lsq_set_row_mask',
            'lsq_set_column_blocks', 'lsq_set_column_blocks_affine', 'lsq_shape', 'lsq_get_csr', 'lsq_release_full_csr',
-           'lsq_solve', 'lsq_spmv', 'lsq_spmv_rows', 'lsq_rows_sumsq', 'lsq_data_colsum', 'lsq_iterate', 'lsq_profile_kernels', 'lsq_cg_available', 'lsq_profile_cg', 'lsq_mg_info', 'lsq_mg_apply', 'lsq_normal_apply', 'lsq_sell_info', 'lsq_sigma_x', 'lsq_cov_band', 'lsq_cov_band_window', 'lsq_cov_band_windows', 'lsq_set_band_order', 'lsq_band_factor',
+           'lsq_solve', 'lsq_spmv', 'lsq_spmv_rows', 'lsq_rows_sumsq', 'lsq_data_colsum', 'lsq_iterate', 'lsq_profile_kernels', 'lsq_cg_available', 'lsq_profile_cg', 'lsq_mg_info', 'lsq_mg_apply', 'lsq_normal_apply', 'lsq_sell_info', 'lsq_sigma_x', 'lsq_cov_band', 'lsq_cov_band_window', 'lsq_cov_band_windows', 'lsq_cov_band_windows_schur', 'lsq_set_band_order', 'lsq_band_factor',
            'lsq_get_rinv', 'lsq_dist_unique_id', 'lsq_create_dist', 'lsq_dist_comm_info', 'lsq_dist_referenced_cols',
            'lsq_dist_set_layout', 'lsq_dist_set_halo', 'lsq_dist_set_global', 'lsq_vgroup_create', 'lsq_vgroup_rank', 'lsq_vgroup_solve', 'lsq_vgroup_iterate',
            'lsq_vgroup_last_error', 'lsq_vgroup_destroy',
@@ -108,6 +108,7 @@ def load():
         'lsq_cov_band': ([P, P, P, ctypes.c_int64, P, P, P, P, P], ctypes.c_int),
         'lsq_cov_band_window': ([P, P, i64, P, P, i64, P, P, P, P, P], ctypes.c_int),
         'lsq_cov_band_windows': ([P, i64, P, P, P, P, P, P, P, P, P, P], ctypes.c_int),
+        'lsq_cov_band_windows_schur': ([P, i64, P, P, P, P, P, P, P, P], ctypes.c_int),
         'lsq_set_band_order': ([P, ctypes.c_int64, P], ctypes.c_int),
         'lsq_band_factor': ([P, P, P, P, P, P], ctypes.c_int),
         'lsq_dist_unique_id': ([P], ctypes.c_int),

@@ -658,6 +658,24 @@ int lsq_cov_band_windows(lsq_handle* h, int64_t n_windows, const int64_t* win_pt
     });
 }
 
+int lsq_cov_band_windows_schur(lsq_handle* h, int64_t n_windows, const int64_t* win_ptr, const int32_t* perm,
+                               const uint8_t* inner, double* E, const int64_t* bot_ptr, const int32_t* bot_perm,
+                               const int64_t* nib, int64_t* info) {
+    return guarded(h, [&](lsq::System& S) {
+        if (!S.G.rp.p) return fail(S, "lsq_cov_band_windows_schur: no matrix");
+        if (S.dist) return fail(S, "lsq_cov_band_windows_schur: not available on distributed handles");
+        if (n_windows < 1 || !win_ptr || !perm || !E || win_ptr[0] != 0 || !bot_ptr || bot_ptr[0] != 0 || !nib ||
+            (bot_ptr[n_windows] > 0 && !bot_perm))
+            return fail(S, "lsq_cov_band_windows_schur: bad windows");
+        for (int64_t w = 0; w < n_windows; ++w)
+            for (int64_t j = bot_ptr[w]; j < bot_ptr[w + 1]; ++j)
+                if (bot_perm[j] < 0 || bot_perm[j] >= S.G.n) return fail(S, "lsq_cov_band_windows_schur: column out of range");
+        lsq::band_cov_windows(S, n_windows, win_ptr, perm, inner, E, nullptr, nullptr, nullptr, nullptr, nullptr, info,
+                              bot_ptr, bot_perm, nib);
+        return 0;
+    });
+}
+
 int lsq_dist_set_global(lsq_handle* h, int64_t n_full, int32_t n_grids, const lsq_grid_desc* grids, int32_t n_stencil,
                         const lsq_stencil_desc* stencils, const int32_t* local_of, int32_t win_row0, int32_t own_row0,
                         int32_t own_row1, int32_t rows) {

@@ -1181,6 +1181,78 @@ void band_cov(System& S, const int32_t* h_perm, int64_t nw, double* h_E, int64_t
 }
 
 
+// ---- a window's bottom margin eliminated first (the Schur split, lsq_cov_band_windows_schur) -----
+// E of a window's interior only needs the factor of the Schur complement of the margin onto the
+// interior: with the columns [Mt (top margin rows), I (interior rows), Mb (bottom margin rows)] and
+// Mt, Mb uncoupled, (N⁻¹)_II = S⁻¹, S = N_II − N_I,Mt N_Mt⁻¹ N_Mt,I − N_I,Mb N_Mb⁻¹ N_Mb,I.  The band
+// factor of A = [Mt, I] (ascending band order) eliminates Mt on the way; Mb's term touches only Ib,
+// the last rows of I that Mb's rows reach: it is taken from the band factor of B' = reverse([Ib, Mb])
+// — Mb eliminated first, the trailing block R_II of that factor has R_IIᵀR_II = N_Ib,Ib − (Mb's
+// term) — and written over A's (Ib, Ib) block before A is factored.  The sweeps of E_j = ‖R_II⁻ᵀe_j‖
+// then stop at the end of I instead of running through Mb: a window's interior rows sit on average
+// half a tile from that end instead of half a tile plus a margin.
+
+// column classes of the window: 1 = A \ Ib, 2 = Ib, 3 = Mb (0: outside)
+__global__ __launch_bounds__(BLOCK) void k_band_cls(int64_t n, const int32_t* __restrict__ perm, int64_t from, int8_t v,
+                                                    int8_t* __restrict__ cls) {
+    for (int64_t j = from + (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLOCK)
+        cls[perm[j]] = v;
+}
+// a live row that holds a column of A \ Ib and one of Mb couples them directly: the split is not
+// exact for this Ib (err = 1)
+__global__ __launch_bounds__(BLOCK) void k_band_schur_check(int64_t m, const int64_t* __restrict__ rp,
+                                                            const int32_t* __restrict__ ci, const int8_t* __restrict__ cls,
+                                                            const double* __restrict__ rs, int* __restrict__ err) {
+    int bad = 0;
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += (int64_t)gridDim.x * BLOCK) {
+        if (rs[i] == 0.0) continue;
+        int has = 0;
+        for (int64_t f = rp[i]; f < rp[i + 1]; ++f) has |= 1 << cls[ci[f]];
+        bad |= (has & 2) && (has & 8);
+    }
+    if (bad) atomicOr(err, 1);
+}
+// A's (Ib, Ib) block ← R_IIᵀR_II of B's factor, unscaled (B's positions [nm, nb) are Ib in
+// descending A order: position p ↔ A position na − 1 − (p − nm)).  One workgroup per pair of B tiles
+// P ≤ Q over [nm, nb); rows below nm of the first tile are masked, tiles outside B's band are 0.
+__global__ __launch_bounds__(BLOCK) void k_band_schur_v(BandDev bb, const double* __restrict__ scb, int64_t nm, int64_t nb,
+                                                        BandDev ba, int64_t na) {
+    __shared__ double SA[TB * LDP], SB[TB * LDP];
+    const int64_t K0 = nm >> 6, nt = bb.T - K0;
+    // pair index -> (P, Q), P ≤ Q, both in [K0, T)
+    int64_t r = blockIdx.x, P = 0;
+    while (r >= nt - P) {
+        r -= nt - P;
+        ++P;
+    }
+    const int64_t Q = P + r;
+    P += K0;
+    const int64_t Qt = Q + K0;
+    if (Qt - P > bb.w) return;   // R_KP and R_KQ never share a row inside the band: the block is 0
+    d4 acc[2][2];
+    acc_zero(acc);
+    for (int64_t K = max<int64_t>(K0, Qt - bb.w); K <= P; ++K) {
+        __syncthreads();
+        const double* tp = btile(bb.R, bb.w, K, P);
+        const double* tq = btile(bb.R, bb.w, K, Qt);
+        for (int idx = threadIdx.x; idx < TT; idx += BLOCK) {
+            const int rr = idx >> 6, c = idx & 63;
+            const bool on = K * TB + rr >= nm;   // rows of eliminated (Mb) columns: not in R_II
+            SA[rr * LDP + c] = on ? tp[idx] : 0.0;
+            SB[rr * LDP + c] = on ? tq[idx] : 0.0;
+        }
+        __syncthreads();
+        mma_tile<true>(SA, SB, acc);
+    }
+    acc_each(acc, [&](int i, int j, double v) {
+        const int64_t p = P * TB + i, q = Qt * TB + j;
+        if (p < nm || q < nm || p >= nb || q >= nb || p > q) return;
+        const double val = v / (scb[p] * scb[q]);
+        const int64_t ap = na - 1 - (p - nm), aq = na - 1 - (q - nm);   // aq ≤ ap
+        btile(ba.R, ba.w, aq >> 6, ap >> 6)[(aq & 63) * TB + (ap & 63)] = val;
+    });
+}
+
 // ---- many windows, pipelined (lsq_cov_band_windows) ------------------------------------------
 // compute_E at scale factors hundreds of windows.  One window's factorization is a chain of T
 // dependent tile steps of 1–w workgroups (latency-bound: the GPU is mostly idle), and its interior
@@ -1193,11 +1265,13 @@ struct BandLane {
     hipStream_t st = nullptr, side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
     DBuf<double> R, D, sc, ring, ssq, dE, dout, ev;
-    DBuf<int32_t> perm, pinv, el;
+    DBuf<double> RB, DB, scB;       // the Schur split's bottom factor (B' = reverse([Ib, Mb]))
+    DBuf<int32_t> perm, pinv, el, permB;
+    DBuf<int8_t> cls;
     DBuf<int64_t> tiles, sp, segK, segE;
     DBuf<int> wmax, err;
     double *hE = nullptr, *hout = nullptr;
-    int* herr = nullptr;
+    int* herr = nullptr;            // [0] factor not positive definite, [1] the split's coupling check
     int64_t capE = 0, capOut = 0;
     // the window whose results are in flight on this lane
     int64_t win = -1, n = 0, nops = 0;
@@ -1222,8 +1296,10 @@ void grow(DBuf<T>& b, int64_t n) {
 void lane_finish(BandLane& L) {
     if (L.win < 0) return;
     HIP_CHECK(hipStreamSynchronize(L.st));
-    if (*L.herr) throw std::invalid_argument("lsq_cov_band_windows: AᵀA of window " + std::to_string(L.win) +
-                                             " is not positive definite (rank-deficient system)");
+    if (L.herr[0]) throw std::invalid_argument("lsq_cov_band_windows: AᵀA of window " + std::to_string(L.win) +
+                                               " is not positive definite (rank-deficient system)");
+    if (L.herr[1]) throw std::domain_error("lsq_cov_band_windows_schur: window " + std::to_string(L.win) +
+                                           " has rows coupling its bottom margin to columns above Ib (a deeper Ib is needed)");
     for (int64_t j = 0; j < L.n; ++j) L.E[j] = (!L.inner || L.inner[j]) ? L.hE[j] : 0.0;
     for (int64_t i = 0; i < L.nops; ++i) L.op_err[i] = std::sqrt(L.hout[i]);
     L.win = -1;
@@ -1232,7 +1308,8 @@ void lane_finish(BandLane& L) {
 
 void band_cov_windows(System& S, int64_t nwin, const int64_t* win_ptr, const int32_t* h_perm, const uint8_t* inner,
                       double* h_E, const int64_t* win_ops, const int64_t* op_ptr, const int32_t* op_pos,
-                      const double* op_val, double* op_err, int64_t* info) {
+                      const double* op_val, double* op_err, int64_t* info, const int64_t* bot_ptr,
+                      const int32_t* bot_perm, const int64_t* nibs) {
     refresh_scaling(S, S.cs_mode < 0 ? 0 : S.cs_mode);
     ensure_full_csr(S);   // the band of AᵀA from G / GT
     const int64_t ncol = S.G.n;
@@ -1263,10 +1340,11 @@ void band_cov_windows(System& S, int64_t nwin, const int64_t* win_ptr, const int
         HIP_CHECK(hipEventCreateWithFlags(&L.join, hipEventDisableTiming));
         HIP_CHECK(hipHostMalloc(&L.hE, sizeof(double) * std::max<int64_t>(nmax, 1)));
         HIP_CHECK(hipHostMalloc(&L.hout, sizeof(double) * std::max<int64_t>(nopad, 1)));
-        HIP_CHECK(hipHostMalloc(&L.herr, sizeof(int)));
+        HIP_CHECK(hipHostMalloc(&L.herr, 2 * sizeof(int)));
         L.pinv.alloc(ncol);
         L.wmax.alloc(1);
-        L.err.alloc(1);
+        L.err.alloc(2);
+        if (bot_ptr) L.cls.alloc(ncol);
     }
     HIP_CHECK(hipStreamSynchronize(S.stream));   // formation / scaling done before the lanes read them
     int64_t products = 0, wmax_all = 0, tmax = 0, dev_bytes = 0;
@@ -1279,9 +1357,55 @@ void band_cov_windows(System& S, int64_t nwin, const int64_t* win_ptr, const int
             const int32_t* perm = h_perm + win_ptr[w];
             const uint8_t* inw = inner ? inner + win_ptr[w] : nullptr;
             hipStream_t st = L.st;
+            L.err.zero(st);
+            // the Schur split (bot_ptr): B' = reverse([Ib, Mb]) factored first; its trailing Ib block
+            // replaces A's (Ib, Ib) block below
+            const int64_t nbw = bot_ptr ? bot_ptr[w + 1] - bot_ptr[w] : 0, nib = nbw > 0 ? nibs[w] : 0, nm = nbw - nib;
+            if (nbw > 0 && (nib < 1 || nm < 1 || nib > n))
+                throw std::invalid_argument("lsq_cov_band_windows_schur: bad bottom part of window " + std::to_string(w));
+            BandDev bB{0, 0, nullptr, nullptr};
+            if (nbw > 0) {
+                const int64_t TBb = (nbw + TB - 1) / TB, npb = TBb * TB;
+                grow(L.permB, nbw);
+                L.permB.upload(bot_perm + bot_ptr[w], nbw, st);
+                HIP_CHECK(hipMemsetAsync(L.pinv.p, 0xff, sizeof(int32_t) * ncol, st));
+                hipLaunchKernelGGL(k_band_pinv, dim3(grid_for(nbw)), dim3(BLOCK), 0, st, nbw, L.permB.p, L.pinv.p);
+                L.wmax.zero(st);
+                hipLaunchKernelGGL(k_band_width, dim3(grid_for(S.G.m)), dim3(BLOCK), 0, st, S.G.m, S.G.rp.p, S.G.ci.p,
+                                   L.pinv.p, S.rs.p, L.wmax.p);
+                KERNEL_CHECK();
+                int hwb = 0;
+                HIP_CHECK(hipMemcpyAsync(&hwb, L.wmax.p, sizeof(int), hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipStreamSynchronize(st));
+                const int bwb = (int)std::min<int64_t>(hwb, TBb - 1);
+                grow(L.RB, TBb * (int64_t)(bwb + 1) * TT);
+                grow(L.DB, TBb * TT);
+                grow(L.scB, npb);
+                bB = BandDev{TBb, bwb, L.RB.p, L.DB.p};
+                HIP_CHECK(hipMemsetAsync(L.RB.p, 0, sizeof(double) * TBb * (bwb + 1) * TT, st));
+                hipLaunchKernelGGL(k_band_normal, dim3(grid_for(npb)), dim3(BLOCK), 0, st, nbw, npb, bB, L.permB.p,
+                                   L.pinv.p, S.GT.rp.p, S.GT.ci.p, S.GT.val.p, S.G.rp.p, S.G.ci.p, S.G.val.p, S.rs.p);
+                hipLaunchKernelGGL(k_band_dscale, dim3(grid_for(npb)), dim3(BLOCK), 0, st, bB, npb, L.scB.p);
+                hipLaunchKernelGGL(k_band_apply_scale, dim3(grid_for(TBb * (bwb + 1) * TT)), dim3(BLOCK), 0, st, bB,
+                                   L.scB.p);
+                KERNEL_CHECK();
+                band_factor_steps(bB, st, L.side, L.fork, L.join, L.err.p);
+            }
             // the window's order on the device and its inverse over every compact column (−1 outside)
             grow(L.perm, n);
             L.perm.upload(perm, n, st);
+            if (nbw > 0) {   // exactness of the split: no live row holds a column of A \ Ib and one of Mb
+                HIP_CHECK(hipMemsetAsync(L.cls.p, 0, ncol, st));
+                hipLaunchKernelGGL(k_band_cls, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, L.perm.p, (int64_t)0, (int8_t)1,
+                                   L.cls.p);
+                hipLaunchKernelGGL(k_band_cls, dim3(grid_for(nib)), dim3(BLOCK), 0, st, n, L.perm.p, n - nib, (int8_t)2,
+                                   L.cls.p);
+                hipLaunchKernelGGL(k_band_cls, dim3(grid_for(nm)), dim3(BLOCK), 0, st, nm, L.permB.p, (int64_t)0,
+                                   (int8_t)3, L.cls.p);
+                hipLaunchKernelGGL(k_band_schur_check, dim3(grid_for(S.G.m)), dim3(BLOCK), 0, st, S.G.m, S.G.rp.p,
+                                   S.G.ci.p, L.cls.p, S.rs.p, L.err.p + 1);
+                KERNEL_CHECK();
+            }
             HIP_CHECK(hipMemsetAsync(L.pinv.p, 0xff, sizeof(int32_t) * ncol, st));
             hipLaunchKernelGGL(k_band_pinv, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, L.perm.p, L.pinv.p);
             L.wmax.zero(st);
@@ -1291,7 +1415,9 @@ void band_cov_windows(System& S, int64_t nwin, const int64_t* win_ptr, const int
             int hw = 0;
             HIP_CHECK(hipMemcpyAsync(&hw, L.wmax.p, sizeof(int), hipMemcpyDeviceToHost, st));
             HIP_CHECK(hipStreamSynchronize(st));   // this lane only: the others keep running
-            const int bw = (int)std::min<int64_t>(hw, T - 1);
+            int bw = (int)std::min<int64_t>(hw, T - 1);
+            if (nbw > 0)   // A's band holds the dense (Ib, Ib) block the split writes
+                bw = (int)std::min<int64_t>(std::max<int64_t>(bw, ((n - 1) >> 6) - ((n - nib) >> 6)), T - 1);
             const int64_t band_tiles = T * (int64_t)(bw + 1);
             // the interior's tiles (the sweeps) and the op rows' sweep plan (positions: no pinv)
             std::vector<int64_t> tiles;
@@ -1341,12 +1467,17 @@ void band_cov_windows(System& S, int64_t nwin, const int64_t* win_ptr, const int
             BandDev b{T, bw, L.R.p, L.D.p};
             hipLaunchKernelGGL(k_band_normal, dim3(grid_for(npad)), dim3(BLOCK), 0, st, n, npad, b, L.perm.p, L.pinv.p,
                                S.GT.rp.p, S.GT.ci.p, S.GT.val.p, S.G.rp.p, S.G.ci.p, S.G.val.p, S.rs.p);
+            if (nbw > 0) {   // (Ib, Ib) ← N_Ib,Ib − N_Ib,Mb N_Mb⁻¹ N_Mb,Ib from B's factor
+                const int64_t ntb = bB.T - (nm >> 6);
+                hipLaunchKernelGGL(k_band_schur_v, dim3((unsigned)(ntb * (ntb + 1) / 2)), dim3(BLOCK), 0, st, bB, L.scB.p,
+                                   nm, nbw, b, n);
+                KERNEL_CHECK();
+            }
             hipLaunchKernelGGL(k_band_dscale, dim3(grid_for(npad)), dim3(BLOCK), 0, st, b, npad, L.sc.p);
             hipLaunchKernelGGL(k_band_apply_scale, dim3(grid_for(band_tiles * TT)), dim3(BLOCK), 0, st, b, L.sc.p);
             KERNEL_CHECK();
-            L.err.zero(st);
             band_factor_steps(b, st, L.side, L.fork, L.join, L.err.p);
-            HIP_CHECK(hipMemcpyAsync(L.herr, L.err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipMemcpyAsync(L.herr, L.err.p, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
             // the diagonal over the interior's tiles, E in window order
             HIP_CHECK(hipMemsetAsync(L.ssq.p, 0, sizeof(double) * npad, st));
             if (nsw > 0) {

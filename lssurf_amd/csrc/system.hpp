@@ -557,7 +557,9 @@ void band_cov(System& S, const int32_t* perm, int64_t nw, double* E, int64_t nop
 // many windows, pipelined over lanes (lsq_cov_band_windows)
 void band_cov_windows(System& S, int64_t nwin, const int64_t* win_ptr, const int32_t* perm, const uint8_t* inner,
                       double* E, const int64_t* win_ops, const int64_t* op_ptr, const int32_t* op_pos,
-                      const double* op_val, double* op_err, int64_t* info);   // rs/cs -> SELL values (single GPU)
+                      const double* op_val, double* op_err, int64_t* info,
+                      const int64_t* bot_ptr = nullptr, const int32_t* bot_perm = nullptr,
+                      const int64_t* nibs = nullptr);   // rs/cs -> SELL values (single GPU)
 void scaling_rows_colnorm(System& S, int precond, bool raw);
 void mf_column_scale(System& S, bool raw);       // lsqr.hip: column norms from the stencil structure
 void scaling_finish_cs(System& S);

@@ -34,6 +34,7 @@ import scipy.sparse as sp
 
 from . import containers as pc
 from .smooth_fit import FitSystem
+from ._native import NativeError
 
 
 def band_order(grids, keep_cols):
@@ -85,9 +86,16 @@ def _node_index(grids, keep_cols):
     return iy[keep_cols], ix[keep_cols]
 
 
-def window_cov(solver, grids, keep_cols, op=None, tile=WINDOW_TILE, margin=WINDOW_MARGIN, timing=None):
+SCHUR_DEPTH = 2   # node rows of the interior the bottom margin's rows reach (AᵀA couples ±2 rows)
+
+
+def window_cov(solver, grids, keep_cols, op=None, tile=WINDOW_TILE, margin=WINDOW_MARGIN, timing=None, schur=None):
     """(E, op_err) of the current weighted, masked system by tiled windows (module docstring):
-    E[c] ≈ sqrt(((AᵀA)⁻¹)_cc) per compact column, op_err[i] ≈ sqrt(op_i (AᵀA)⁻¹ op_iᵀ)."""
+    E[c] ≈ sqrt(((AᵀA)⁻¹)_cc) per compact column, op_err[i] ≈ sqrt(op_i (AᵀA)⁻¹ op_iᵀ).
+
+    schur (default: on when there are no op rows; LSQ_E_SCHUR=0 turns it off): each window's bottom
+    margin is eliminated first (lsq_cov_band_windows_schur) — the same conditional variance, with
+    the sweeps ending at the interior instead of the window's end (DESIGN.md §Error propagation)."""
     iy, ix = _node_index(grids, keep_cols)
     order = band_order(grids, keep_cols)
     n = iy.size
@@ -115,6 +123,10 @@ def window_cov(solver, grids, keep_cols, op=None, tile=WINDOW_TILE, margin=WINDO
     # window's rows are one contiguous run of it, filtered by node column (round 5: the full-length
     # masks and the n-long E of every window were ~0.2 s of host work per window at C4)
     rows_sorted = bool(np.all(iy_o[1:] >= iy_o[:-1]))
+    if schur is None:
+        schur = op is None and os.environ.get('LSQ_E_SCHUR', '1') != '0'
+    schur = bool(schur) and rows_sorted and op is None
+    depth = SCHUR_DEPTH
 
     def window(y0, y1, x0, x1):   # band-order positions of the nodes [y0, y1) × [x0, x1)
         a, b = (np.searchsorted(iy_o, y0, 'left'), np.searchsorted(iy_o, y1, 'left')) if rows_sorted else (0, n)
@@ -129,9 +141,18 @@ def window_cov(solver, grids, keep_cols, op=None, tile=WINDOW_TILE, margin=WINDO
     # small spec; its positions are formed only when its batch goes to the device
     # (lsq_cov_band_windows), so host memory stays O(WINDOW_BATCH windows) whatever the grid
     def tile_win(ty, tx, mg):
-        pos = window(ty - mg, ty + tile + mg, tx - mg, tx + tile + mg)
+        if schur:   # A = [top margin, interior] rows; B' = reverse([Ib, bottom margin] rows)
+            yb = min(ty + tile, ny)
+            pos = window(ty - mg, yb, tx - mg, tx + tile + mg)
+            bot = window(yb - depth, ty + tile + mg, tx - mg, tx + tile + mg)[::-1] if yb < ny else None
+            nib = int(np.count_nonzero(iy_o[pos] >= yb - depth))
+            if bot is not None and (bot.size <= nib or nib == 0):
+                bot = None
+        else:
+            pos = window(ty - mg, ty + tile + mg, tx - mg, tx + tile + mg)
+            bot, nib = None, 0
         yi, xi = iy_o[pos], ix_o[pos]
-        return pos, (yi >= ty) & (yi < ty + tile) & (xi >= tx) & (xi < tx + tile)
+        return pos, (yi >= ty) & (yi < ty + tile) & (xi >= tx) & (xi < tx + tile), bot, nib
 
     specs = [('tile', ty, tx) for ty in range(0, ny, tile) for tx in range(0, nx, tile)]
     ntiles = len(specs)
@@ -144,17 +165,17 @@ def window_cov(solver, grids, keep_cols, op=None, tile=WINDOW_TILE, margin=WINDO
     m2 = 2 * margin
     specs.append(('check', cy, cx))
 
-    def materialize(spec):   # (positions, inner flags or None, op rows or None)
+    def materialize(spec):   # (positions, inner flags or None, op rows or None, B' positions or None, nib)
         if spec[0] == 'tile':
             ty, tx = spec[1], spec[2]
-            pos, inner = tile_win(ty, tx, margin)
+            pos, inner, bot, nib = tile_win(ty, tx, margin)
             rows = None if op is None else np.flatnonzero((oty == ty // tile) & (otx == tx // tile) & ~own)
-            return pos, inner, rows
+            return pos, inner, rows, bot, nib
         if spec[0] == 'own':
             b = spec[1]
-            return window(b[0] - margin, b[1] + margin + 1, b[2] - margin, b[3] + margin + 1), None, spec[2]
-        pos, inner = tile_win(spec[1], spec[2], m2)
-        return pos, inner, None
+            return window(b[0] - margin, b[1] + margin + 1, b[2] - margin, b[3] + margin + 1), None, spec[2], None, 0
+        pos, inner, bot, nib = tile_win(spec[1], spec[2], m2)
+        return pos, inner, None, bot, nib
 
     E2 = pos2 = inner2 = None
     wmax = products = 0
@@ -164,10 +185,26 @@ def window_cov(solver, grids, keep_cols, op=None, tile=WINDOW_TILE, margin=WINDO
         chunk = [materialize(sp_) for sp_ in specs[c0:c0 + batch]]
         req = [(order[pos], inner if inner is not None else np.zeros(pos.size, bool),
                 op[rows] if (op is not None and rows is not None and rows.size) else None)
-               for pos, inner, rows in chunk]
-        Es, oes, info = solver.cov_band_windows(req)
+               for pos, inner, rows, _, _ in chunk]
+        if schur:
+            while True:
+                sreq = [(cols, inn, None if bot is None else order[bot], nib)
+                        for (cols, inn, _), (_, _, _, bot, nib) in zip(req, chunk)]
+                try:
+                    Es, info = solver.cov_band_windows_schur(sreq)
+                    break
+                except NativeError as e:   # a row reaches further than Ib: split one node row deeper
+                    if 'deeper Ib' not in str(e) or depth >= 2 * SCHUR_DEPTH:
+                        raise
+                    depth += 1
+                    chunk = [materialize(sp_) for sp_ in specs[c0:c0 + batch]]
+                    req = [(order[pos], inner if inner is not None else np.zeros(pos.size, bool), None)
+                           for pos, inner, _, _, _ in chunk]
+            oes = [None] * len(chunk)
+        else:
+            Es, oes, info = solver.cov_band_windows(req)
         wmax, products = max(wmax, int(info[0])), products + int(info[3])
-        for k, ((pos, inner, rows), (cols, _, _), Et, oe) in enumerate(zip(chunk, req, Es, oes)):
+        for k, ((pos, inner, rows, _, _), (cols, _, _), Et, oe) in enumerate(zip(chunk, req, Es, oes)):
             if c0 + k == len(specs) - 1:       # the self-check window
                 E2, pos2, inner2 = Et, pos, inner
                 continue
@@ -186,7 +223,7 @@ def window_cov(solver, grids, keep_cols, op=None, tile=WINDOW_TILE, margin=WINDO
         timing['E_window'] = {'tiles': ntiles, 'op_windows': nown, 'tile': tile, 'margin': margin,
                               'max_band_tiles': wmax, 'tile_products': products, 'selfcheck_rel': check,
                               'selfcheck_margin': m2, 'time_s': time() - t_all, 'lanes': int(info[5]),
-                              'batch': batch}
+                              'batch': batch, 'schur': bool(schur), 'schur_depth': depth if schur else None}
     return E, op_err, check
 
 

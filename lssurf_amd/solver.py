@@ -210,7 +210,13 @@ class LSQSolver:
         o = np.zeros(1 + 4 * 32, np.int64)
         self._check(self._L.lsq_mg_info(self._h, ptr(o), o.size), 'lsq_mg_info')
         L = int(o[0])
+        self._mg_tail = int(o[1 + 4 * L])
         return [tuple(int(v) for v in o[1 + 4 * l:4 + 4 * l]) for l in range(L)], int(o[4])
+
+    def mg_tail_level(self):
+        """First level of the multigrid's one-workgroup tail V-cycle (k_mg_tail), −1 for none."""
+        self.mg_info()
+        return self._mg_tail
 
     def mg_apply(self, level, what, x=None):
         """Multigrid test hook: what 0 → N_l x on level l's full column space; 1 → V-cycle(x)
@@ -381,6 +387,28 @@ class LSQSolver:
                     'lsq_cov_band_windows')
         return ([E[wp[i]:wp[i + 1]] for i in range(len(windows))],
                 [oe[wo[i]:wo[i + 1]] if nrow[i] else None for i in range(len(windows))], info)
+
+    def cov_band_windows_schur(self, windows):
+        """cov_band_windows with each window's bottom margin eliminated first
+        (lsq_cov_band_windows_schur): windows = [(perm_A, inner_A, perm_B or None, nib)], perm_A =
+        [top margin, interior] rows ascending ending with the nib columns of Ib, perm_B = the band
+        order of [Ib, bottom margin] reversed.  Returns ([E_w over perm_A], info)."""
+        sa = [len(w[0]) for w in windows]
+        sb = [0 if w[2] is None else len(w[2]) for w in windows]
+        wp = as_c(np.r_[0, np.cumsum(sa)], np.int64)
+        bp = as_c(np.r_[0, np.cumsum(sb)], np.int64)
+        perm = as_c(np.concatenate([np.asarray(w[0]) for w in windows]), np.int32)
+        inner = as_c(np.concatenate([np.ones(n, bool) if w[1] is None else np.asarray(w[1], bool)
+                                     for w, n in zip(windows, sa)]), np.uint8)
+        bperm = as_c(np.concatenate([np.asarray(w[2]) for w in windows if w[2] is not None] or [np.zeros(0)]),
+                     np.int32)
+        nib = as_c(np.array([w[3] if w[2] is not None else 0 for w in windows]), np.int64)
+        E = np.zeros(perm.size)
+        info = np.zeros(6, np.int64)
+        self._check(self._L.lsq_cov_band_windows_schur(self._h, len(windows), ptr(wp), ptr(perm), ptr(inner), ptr(E),
+                                                       ptr(bp), ptr(bperm), ptr(nib), ptr(info)),
+                    'lsq_cov_band_windows_schur')
+        return [E[wp[i]:wp[i + 1]] for i in range(len(windows))], info
 
     def spmv(self, x, trans=False):
         """G x (trans False) or Gᵀ x on the UNWEIGHTED formed operator, all rows."""

@@ -156,3 +156,40 @@ def test_batched_windows_equal_single_windows(gpu_available, lanes):
             os.environ.pop('LSQ_E_LANES', None)
         else:
             os.environ['LSQ_E_LANES'] = saved
+
+
+def _golden_system(name):
+    from lssurf_amd.constraint_functions import reference_epoch_keep_cols
+    from lssurf_amd.smooth_fit import FitSystem
+    g = golden(f'sys_{name}.npz')
+    kw = golden_kwargs(g)
+    kw['VERBOSE'] = False
+    S = LS.smooth_fit(data=golden_points(g), return_fit_objects=True, **kw)
+    keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch'])
+    fs = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, grids=S['grids'])
+    w = 1. / np.concatenate((S['Ed'], S['Ec']))
+    fs.solver.set_row_weight(w)
+    fs.solver.set_row_mask(np.ones(w.size, bool))
+    return S, fs, keep
+
+
+@pytest.mark.parametrize('name,tile,margin', [('t128', 32, 24), ('sf3d_edit', 4, 3), ('deep1', 16, 8)])
+def test_window_schur_split_equals_whole_window(gpu_available, name, tile, margin):
+    """The Schur split (each window's bottom margin eliminated first, lsq_cov_band_windows_schur)
+    is the same conditional variance as the whole window's band factor: equal to rounding, on the
+    BASELINE layout (t128), z0 on a 2× refinement of the dz lattice (sf3d_edit) and the depth
+    golden's lattice (deep1) — and its sweeps are fewer."""
+    from lssurf_amd.errors import window_cov
+    S, fs, keep = _golden_system(name) if name.startswith(('sf3d', 'deep')) else _system(name)
+    try:
+        t0, t1 = {}, {}
+        Ew, _, c0 = window_cov(fs.solver, S['grids'], keep, tile=tile, margin=margin, schur=False, timing=t0)
+        Es, _, c1 = window_cov(fs.solver, S['grids'], keep, tile=tile, margin=margin, schur=True, timing=t1)
+    finally:
+        fs.close()
+    assert t1['E_window']['schur'] and not t0['E_window']['schur']
+    assert np.all(Ew > 0)
+    rel = np.abs(Es - Ew) / Ew
+    assert rel.max() <= 1e-9, rel.max()
+    assert abs(c1 - c0) <= 1e-9 + 1e-6 * abs(c0)
+    assert t1['E_window']['tile_products'] < t0['E_window']['tile_products']

@@ -32,6 +32,9 @@ def main(cfg):
     import hashlib
     import numpy as np
     digest = hashlib.sha256(np.ascontiguousarray(np.asarray(sz, dtype=np.float64)).tobytes()).hexdigest()[:16]
+    import os
+    if os.environ.get('LSQ_E_SAVE'):   # σ grids for a comparison between switches (npz)
+        np.savez(os.environ['LSQ_E_SAVE'], sigma_z0=np.asarray(sz), sigma_dz=np.asarray(S['E']['sigma_dz'].sigma_dz))
     print(json.dumps({'config': cfg, 'wall_s': wall, 'timing': tim,
                       'sigma_z0_median': float(sorted(sz.ravel())[sz.size // 2]),
                       'sigma_z0_sha16': digest,   # bit-level identity of σ_z0 between builds / switches
