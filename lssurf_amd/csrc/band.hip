@@ -26,6 +26,7 @@
 #include <chrono>
 #include <algorithm>
 #include <climits>
+#include <memory>
 #include <cmath>
 #include <stdexcept>
 #include <vector>
@@ -212,7 +213,7 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 // thread per trailing column), the trailing triangle's rank-16 update by all 256 threads — 12
 // barriers.  (Unblocked: one wave with readlane, 68 µs per tile; 256 threads with a barrier per
 // elimination step, 128 µs.)  The lower triangle is zeroed.
-__global__ __launch_bounds__(BLOCK) void k_band_potrf(BandDev b, int64_t K, int* err) {
+__device__ __forceinline__ void band_potrf_body(const BandDev& b, int64_t K, int* err) {
     __shared__ double A[TB * LDP];
     __shared__ double rinv[TB];
     __shared__ int bad;
@@ -283,11 +284,16 @@ __global__ __launch_bounds__(BLOCK) void k_band_potrf(BandDev b, int64_t K, int*
         Rt[idx] = c >= r ? A[r * LDP + c] : 0.0;
     }
 }
+__global__ __launch_bounds__(BLOCK) void k_band_potrf(BandDev b, int64_t K, int* err) { band_potrf_body(b, K, err); }
+// a batch of bands (compute_E windows): band blockIdx.y, its error flag errs[2·y]
+__global__ __launch_bounds__(BLOCK) void k_band_potrf_b(const BandDev* __restrict__ bs, int64_t K, int* errs) {
+    const BandDev b = bs[blockIdx.y];
+    if (K < b.T) band_potrf_body(b, K, errs + 2 * blockIdx.y);
+}
 
 // D_K = R_KK⁻¹ for every tile row at once (one wave per tile, lane k: column k by back
 // substitution, R's rows broadcast with readlane)
-__global__ __launch_bounds__(TB) void k_band_dinv(BandDev b) {
-    const int64_t K = blockIdx.x;
+__device__ __forceinline__ void band_dinv_body(const BandDev& b, int64_t K) {
     const int k = threadIdx.x;
     const double* Rt = btile(b.R, b.w, K, K);
     double a[TB];
@@ -305,17 +311,22 @@ __global__ __launch_bounds__(TB) void k_band_dinv(BandDev b) {
 #pragma unroll
     for (int i = 0; i < TB; ++i) Dk[i * TB + k] = x[i];
 }
+__global__ __launch_bounds__(TB) void k_band_dinv(BandDev b) { band_dinv_body(b, blockIdx.x); }
+__global__ __launch_bounds__(TB) void k_band_dinv_b(const BandDev* __restrict__ bs) {
+    const BandDev b = bs[blockIdx.y];
+    if ((int64_t)blockIdx.x < b.T) band_dinv_body(b, blockIdx.x);
+}
 
 // R_KJ = R_KK⁻ᵀ N_KJ for J = K+1..K+m (one workgroup per tile), blocked by 16 rows: the 16 rows
 // of a block by substitution (a thread per column), then the rows below updated with them by all
 // 256 threads — 8 barriers.  Multiplying by the explicit D_Kᵀ instead would lose ~cond(R_KK)·ε
 // per tile row.
-__global__ __launch_bounds__(BLOCK) void k_band_trsm(BandDev b, int64_t K) {
+__device__ __forceinline__ void band_trsm_body(const BandDev& b, int64_t K, int bx) {
     __shared__ double R[TB * LDP];
     __shared__ double X[TB * LDP];
     __shared__ double rinv[TB];
     const double* Rkk = btile(b.R, b.w, K, K);
-    double* Nt = btile(b.R, b.w, K, K + 1 + blockIdx.x);
+    double* Nt = btile(b.R, b.w, K, K + 1 + bx);
     for (int idx = threadIdx.x; idx < TT; idx += BLOCK) {
         const int r = idx >> 6, c = idx & 63;
         R[r * LDP + c] = Rkk[idx];
@@ -352,22 +363,28 @@ __global__ __launch_bounds__(BLOCK) void k_band_trsm(BandDev b, int64_t K) {
     }
     for (int idx = threadIdx.x; idx < TT; idx += BLOCK) Nt[idx] = X[(idx >> 6) * LDP + (idx & 63)];
 }
+__global__ __launch_bounds__(BLOCK) void k_band_trsm(BandDev b, int64_t K) { band_trsm_body(b, K, blockIdx.x); }
+__global__ __launch_bounds__(BLOCK) void k_band_trsm_b(const BandDev* __restrict__ bs, int64_t K) {
+    const BandDev b = bs[blockIdx.y];
+    if (K < b.T && (int64_t)blockIdx.x < std::min<int64_t>(b.w, b.T - 1 - K)) band_trsm_body(b, K, blockIdx.x);
+}
 
 // N_{K+a, K+c} −= R_{K,K+a}ᵀ R_{K,K+c}, 1 ≤ a ≤ c ≤ m, one workgroup per pair.  ROW: only the
 // next tile row (a = 1, c = 1 + blockIdx.x) — the look-ahead the next POTRF/TRSM wait for;
 // otherwise the rest (2 ≤ a ≤ c ≤ m, (m−1)m/2 workgroups), which runs beside them on a second
 // stream.  (A square m² grid with the lower pairs idle cost ~2× in dispatch at w = 65.)
 template <bool ROW>
-__global__ __launch_bounds__(BLOCK) void k_band_syrk(BandDev b, int64_t K, int m) {
-    int a = 1, c = 1 + (int)blockIdx.x;
+__device__ __forceinline__ void band_syrk_body(const BandDev& b, int64_t K, int m, int bx) {
+    int a = 1, c = 1 + bx;
     if (!ROW) {
-        const int p = blockIdx.x;
+        const int p = bx;
         int c0 = (int)((sqrt(8.0 * p + 1.0) - 1.0) * 0.5);
         while ((c0 + 1) * (c0 + 2) / 2 <= p) ++c0;
         while (c0 * (c0 + 1) / 2 > p) --c0;
         a = p - c0 * (c0 + 1) / 2 + 2;
         c = c0 + 2;
     }
+    if (c > m) return;   // a batch's band with fewer trailing tiles than the launch's widest
     __shared__ double A[TB * LDP];
     __shared__ double B[TB * LDP];
     TilePair tp;   // both tiles' loads in flight together; A used transposed in place (no LDS transpose)
@@ -379,6 +396,13 @@ __global__ __launch_bounds__(BLOCK) void k_band_syrk(BandDev b, int64_t K, int m
     mma_tile<true>(A, B, acc);
     double* Ct = btile(b.R, b.w, K + a, K + c);
     acc_each(acc, [&](int r, int cc, double v) { Ct[r * TB + cc] -= v; });
+}
+template <bool ROW>
+__global__ __launch_bounds__(BLOCK) void k_band_syrk(BandDev b, int64_t K, int m) { band_syrk_body<ROW>(b, K, m, blockIdx.x); }
+template <bool ROW>
+__global__ __launch_bounds__(BLOCK) void k_band_syrk_b(const BandDev* __restrict__ bs, int64_t K) {
+    const BandDev b = bs[blockIdx.y];
+    if (K < b.T) band_syrk_body<ROW>(b, K, (int)std::min<int64_t>(b.w, b.T - 1 - K), blockIdx.x);
 }
 
 // y = R⁻ᵀ o for the 64 right-hand sides of one workgroup, tile row by tile row from the first
@@ -886,6 +910,38 @@ void band_factor_steps(const BandDev& b, hipStream_t st, hipStream_t side, hipEv
     KERNEL_CHECK();
 }
 
+// The same steps for a batch of independent bands (compute_E's windows): one launch per kernel
+// and step serves every band of the batch (blockIdx.y), so the chain's latency — a window's
+// factorization is T dependent steps of 1–w workgroups — is paid once per batch, not per window.
+// d_bs: the bands on the device, bs: the same on the host; errs: 2 ints per band ([0] pivot).
+void band_factor_steps_batch(const BandDev* d_bs, const std::vector<BandDev>& bs, hipStream_t st, hipStream_t side,
+                             hipEvent_t fork, hipEvent_t join, int* errs) {
+    const unsigned nb = (unsigned)bs.size();
+    int64_t Tmax = 0;
+    for (const BandDev& b : bs) Tmax = std::max(Tmax, b.T);
+    HIP_CHECK(hipEventRecord(join, st));
+    for (int64_t K = 0; K < Tmax; ++K) {
+        hipLaunchKernelGGL(k_band_potrf_b, dim3(1, nb), dim3(BLOCK), 0, st, d_bs, K, errs);
+        int m = 0;
+        for (const BandDev& b : bs)
+            if (K < b.T) m = std::max<int>(m, (int)std::min<int64_t>(b.w, b.T - 1 - K));
+        if (m > 0) {
+            hipLaunchKernelGGL(k_band_trsm_b, dim3(m, nb), dim3(BLOCK), 0, st, d_bs, K);
+            HIP_CHECK(hipStreamWaitEvent(st, join, 0));
+            hipLaunchKernelGGL(k_band_syrk_b<true>, dim3(m, nb), dim3(BLOCK), 0, st, d_bs, K);
+            if (m > 1) {
+                HIP_CHECK(hipEventRecord(fork, st));
+                HIP_CHECK(hipStreamWaitEvent(side, fork, 0));
+                hipLaunchKernelGGL(k_band_syrk_b<false>, dim3((m - 1) * m / 2, nb), dim3(BLOCK), 0, side, d_bs, K);
+                HIP_CHECK(hipEventRecord(join, side));
+            }
+        }
+    }
+    HIP_CHECK(hipStreamWaitEvent(st, join, 0));
+    hipLaunchKernelGGL(k_band_dinv_b, dim3((unsigned)Tmax, nb), dim3(TB), 0, st, d_bs);
+    KERNEL_CHECK();
+}
+
 __global__ __launch_bounds__(BLOCK) void k_band_pinv(int64_t n, const int32_t* __restrict__ perm,
                                                      int32_t* __restrict__ pinv) {
     for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLOCK) pinv[perm[j]] = (int32_t)j;
@@ -1306,6 +1362,268 @@ void lane_finish(BandLane& L) {
 }
 }  // namespace
 
+// ---- windows in batches: one factorization chain for several windows -----------------------------
+// band_cov_windows runs one window's factorization per lane: T dependent steps of small launches
+// (C4: ~1 300 steps of ~70 µs per 80-node window), so the chain's latency, not its flops, sets the
+// time (round 5, serial: 93 s of factorization for 1 024 windows).  Here a lane takes LSQ_E_FBATCH
+// windows at once: each window's band is assembled as before, then every step's POTRF / TRSM /
+// SYRK launch serves the whole batch (band_factor_steps_batch) — first the bottom parts B' of the
+// Schur split, then the A parts — and each window's sweeps follow.  Identity sweeps only (no op
+// rows); the same sums as band_cov_windows, bit for bit.
+namespace {
+struct BatchSlot {
+    DBuf<double> R, D, sc, RB, DB, scB, dE;
+    DBuf<int32_t> perm, permB;
+    double* hE = nullptr;
+    int64_t capE = 0;
+    int64_t win = -1, n = 0;
+    double* E = nullptr;
+    const uint8_t* inner = nullptr;
+    ~BatchSlot() {
+        if (hE) (void)hipHostFree(hE);
+    }
+};
+struct BatchLane {
+    hipStream_t st = nullptr, side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    DBuf<int32_t> pinv;
+    DBuf<int8_t> cls;
+    DBuf<int> wmax, errs, errsB;
+    DBuf<double> ring, ssq;
+    DBuf<int64_t> tiles;
+    DBuf<BandDev> dA, dB;
+    std::unique_ptr<BatchSlot[]> slots;
+    std::vector<int64_t> bslot;   // the batch's B' bands: slot of each
+    int* herr = nullptr;          // [0, 2·nb): A's flags per slot, [2·nb, 4·nb): B''s per B' band
+    int nin = 0;
+    ~BatchLane() {
+        if (herr) (void)hipHostFree(herr);
+        if (fork) (void)hipEventDestroy(fork);
+        if (join) (void)hipEventDestroy(join);
+        if (st) (void)hipStreamDestroy(st);
+        if (side) (void)hipStreamDestroy(side);
+    }
+};
+void batch_finish(BatchLane& L, int nbmax) {
+    if (L.nin == 0) return;
+    HIP_CHECK(hipStreamSynchronize(L.st));
+    for (int i = 0; i < L.nin; ++i) {
+        BatchSlot& W = L.slots[i];
+        if (L.herr[2 * i]) throw std::invalid_argument("lsq_cov_band_windows: AᵀA of window " + std::to_string(W.win) +
+                                                       " is not positive definite (rank-deficient system)");
+        if (L.herr[2 * i + 1]) throw std::domain_error("lsq_cov_band_windows_schur: window " + std::to_string(W.win) +
+                                                       " has rows coupling its bottom margin to columns above Ib (a deeper Ib is needed)");
+    }
+    for (size_t k = 0; k < L.bslot.size(); ++k)
+        if (L.herr[2 * nbmax + 2 * k])
+            throw std::invalid_argument("lsq_cov_band_windows: the bottom part of window " +
+                                        std::to_string(L.slots[L.bslot[k]].win) + " is not positive definite");
+    for (int i = 0; i < L.nin; ++i) {
+        BatchSlot& W = L.slots[i];
+        for (int64_t j = 0; j < W.n; ++j) W.E[j] = (!W.inner || W.inner[j]) ? W.hE[j] : 0.0;
+        W.win = -1;
+    }
+    L.nin = 0;
+}
+// a band's width over the lane's current pinv (host readback: this lane's stream only)
+int band_width_of(System& S, BatchLane& L, int64_t T) {
+    L.wmax.zero(L.st);
+    hipLaunchKernelGGL(k_band_width, dim3(grid_for(S.G.m)), dim3(BLOCK), 0, L.st, S.G.m, S.G.rp.p, S.G.ci.p, L.pinv.p,
+                       S.rs.p, L.wmax.p);
+    KERNEL_CHECK();
+    int hw = 0;
+    HIP_CHECK(hipMemcpyAsync(&hw, L.wmax.p, sizeof(int), hipMemcpyDeviceToHost, L.st));
+    HIP_CHECK(hipStreamSynchronize(L.st));
+    return (int)std::min<int64_t>(hw, T - 1);
+}
+// AᵀA of the columns perm[0, n) into band b (the lane's pinv set for them), equilibrated into sc
+void band_assemble(System& S, BatchLane& L, const BandDev& b, int64_t n, const int32_t* perm, double* sc,
+                   const BandDev* schur_from = nullptr, const double* scb = nullptr, int64_t nm = 0, int64_t nbw = 0) {
+    const int64_t npad = b.T * TB;
+    HIP_CHECK(hipMemsetAsync(b.R, 0, sizeof(double) * b.T * (b.w + 1) * TT, L.st));
+    hipLaunchKernelGGL(k_band_normal, dim3(grid_for(npad)), dim3(BLOCK), 0, L.st, n, npad, b, perm, L.pinv.p, S.GT.rp.p,
+                       S.GT.ci.p, S.GT.val.p, S.G.rp.p, S.G.ci.p, S.G.val.p, S.rs.p);
+    if (schur_from) {
+        const int64_t ntb = schur_from->T - (nm >> 6);
+        hipLaunchKernelGGL(k_band_schur_v, dim3((unsigned)(ntb * (ntb + 1) / 2)), dim3(BLOCK), 0, L.st, *schur_from, scb,
+                           nm, nbw, b, n);
+    }
+    hipLaunchKernelGGL(k_band_dscale, dim3(grid_for(npad)), dim3(BLOCK), 0, L.st, b, npad, sc);
+    hipLaunchKernelGGL(k_band_apply_scale, dim3(grid_for(b.T * (b.w + 1) * TT)), dim3(BLOCK), 0, L.st, b, sc);
+    KERNEL_CHECK();
+}
+}  // namespace
+
+void band_cov_windows_batched(System& S, int64_t nwin, const int64_t* win_ptr, const int32_t* h_perm,
+                              const uint8_t* inner, double* h_E, int64_t* info, const int64_t* bot_ptr,
+                              const int32_t* bot_perm, const int64_t* nibs, int nbmax) {
+    const int64_t ncol = S.G.n;
+    const int nl = [] {
+        const char* e = getenv("LSQ_E_LANES");
+        return e ? std::max(1, std::min(atoi(e), 8)) : 2;
+    }();
+    std::vector<BatchLane> lanes(nl);
+    for (BatchLane& L : lanes) {
+        HIP_CHECK(hipStreamCreateWithFlags(&L.st, hipStreamNonBlocking));
+        HIP_CHECK(hipStreamCreateWithFlags(&L.side, hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&L.fork, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&L.join, hipEventDisableTiming));
+        HIP_CHECK(hipHostMalloc(&L.herr, sizeof(int) * 4 * nbmax));
+        L.pinv.alloc(ncol);
+        if (bot_ptr) L.cls.alloc(ncol);
+        L.wmax.alloc(1);
+        L.errs.alloc(2 * nbmax);
+        L.errsB.alloc(2 * nbmax);
+        L.dA.alloc(nbmax);
+        L.dB.alloc(nbmax);
+        L.slots.reset(new BatchSlot[nbmax]);
+    }
+    HIP_CHECK(hipStreamSynchronize(S.stream));
+    int64_t products = 0, wmax_all = 0, tmax = 0, dev_bytes = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    try {
+        int64_t batch = 0;
+        for (int64_t w0 = 0; w0 < nwin; w0 += nbmax, ++batch) {
+            BatchLane& L = lanes[batch % nl];
+            batch_finish(L, nbmax);
+            const int nb = (int)std::min<int64_t>(nbmax, nwin - w0);
+            hipStream_t st = L.st;
+            L.errs.zero(st);
+            L.errsB.zero(st);
+            // 1. the bottom parts B' (Schur split), then their factorization as one batch
+            std::vector<BandDev> hb, ha(nb);
+            std::vector<int64_t> nms(nb, 0), nbws(nb, 0);
+            std::vector<int> bidx(nb, -1);
+            L.bslot.clear();
+            for (int i = 0; i < nb; ++i) {
+                const int64_t w = w0 + i, n = win_ptr[w + 1] - win_ptr[w];
+                BatchSlot& W = L.slots[i];
+                const int64_t nbw = bot_ptr ? bot_ptr[w + 1] - bot_ptr[w] : 0, nib = nbw > 0 ? nibs[w] : 0;
+                if (nbw > 0 && (nib < 1 || nbw - nib < 1 || nib > n))
+                    throw std::invalid_argument("lsq_cov_band_windows_schur: bad bottom part of window " + std::to_string(w));
+                nbws[i] = nbw;
+                nms[i] = nbw - nib;
+                if (nbw == 0) continue;
+                const int64_t TBb = (nbw + TB - 1) / TB;
+                grow(W.permB, nbw);
+                W.permB.upload(bot_perm + bot_ptr[w], nbw, st);
+                HIP_CHECK(hipMemsetAsync(L.pinv.p, 0xff, sizeof(int32_t) * ncol, st));
+                hipLaunchKernelGGL(k_band_pinv, dim3(grid_for(nbw)), dim3(BLOCK), 0, st, nbw, W.permB.p, L.pinv.p);
+                const int bwb = band_width_of(S, L, TBb);
+                grow(W.RB, TBb * (int64_t)(bwb + 1) * TT);
+                grow(W.DB, TBb * TT);
+                grow(W.scB, TBb * TB);
+                const BandDev bB{TBb, bwb, W.RB.p, W.DB.p};
+                band_assemble(S, L, bB, nbw, W.permB.p, W.scB.p);
+                bidx[i] = (int)hb.size();
+                hb.push_back(bB);
+                L.bslot.push_back(i);
+            }
+            if (!hb.empty()) {
+                L.dB.upload(hb.data(), (int64_t)hb.size(), st);
+                band_factor_steps_batch(L.dB.p, hb, st, L.side, L.fork, L.join, L.errsB.p);
+            }
+            // 2. the A parts: the split's coupling check, AᵀA with the Schur block, one factorization
+            for (int i = 0; i < nb; ++i) {
+                const int64_t w = w0 + i, n = win_ptr[w + 1] - win_ptr[w], T = (n + TB - 1) / TB;
+                BatchSlot& W = L.slots[i];
+                grow(W.perm, n);
+                W.perm.upload(h_perm + win_ptr[w], n, st);
+                const int64_t nbw = nbws[i], nm = nms[i], nib = nbw - nm;
+                if (nbw > 0) {
+                    HIP_CHECK(hipMemsetAsync(L.cls.p, 0, ncol, st));
+                    hipLaunchKernelGGL(k_band_cls, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, W.perm.p, (int64_t)0,
+                                       (int8_t)1, L.cls.p);
+                    hipLaunchKernelGGL(k_band_cls, dim3(grid_for(nib)), dim3(BLOCK), 0, st, n, W.perm.p, n - nib,
+                                       (int8_t)2, L.cls.p);
+                    hipLaunchKernelGGL(k_band_cls, dim3(grid_for(nm)), dim3(BLOCK), 0, st, nm, W.permB.p, (int64_t)0,
+                                       (int8_t)3, L.cls.p);
+                    hipLaunchKernelGGL(k_band_schur_check, dim3(grid_for(S.G.m)), dim3(BLOCK), 0, st, S.G.m, S.G.rp.p,
+                                       S.G.ci.p, L.cls.p, S.rs.p, L.errs.p + 2 * i + 1);
+                    KERNEL_CHECK();
+                }
+                HIP_CHECK(hipMemsetAsync(L.pinv.p, 0xff, sizeof(int32_t) * ncol, st));
+                hipLaunchKernelGGL(k_band_pinv, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, W.perm.p, L.pinv.p);
+                int bw = band_width_of(S, L, T);
+                if (nbw > 0) bw = (int)std::min<int64_t>(std::max<int64_t>(bw, ((n - 1) >> 6) - ((n - nib) >> 6)), T - 1);
+                grow(W.R, T * (int64_t)(bw + 1) * TT);
+                grow(W.D, T * TT);
+                grow(W.sc, T * TB);
+                grow(W.dE, n);
+                ha[i] = BandDev{T, bw, W.R.p, W.D.p};
+                if (nbw > 0) band_assemble(S, L, ha[i], n, W.perm.p, W.sc.p, &hb[bidx[i]], W.scB.p, nm, nbw);
+                else band_assemble(S, L, ha[i], n, W.perm.p, W.sc.p);
+                wmax_all = std::max<int64_t>(wmax_all, bw);
+                tmax = std::max(tmax, T);
+            }
+            L.dA.upload(ha.data(), nb, st);
+            band_factor_steps_batch(L.dA.p, ha, st, L.side, L.fork, L.join, L.errs.p);
+            // 3. each window's sweeps over the tiles holding an inner position
+            for (int i = 0; i < nb; ++i) {
+                const int64_t w = w0 + i, n = win_ptr[w + 1] - win_ptr[w], T = ha[i].T;
+                const uint8_t* inw = inner ? inner + win_ptr[w] : nullptr;
+                BatchSlot& W = L.slots[i];
+                std::vector<int64_t> tiles;
+                for (int64_t J = 0; J < T; ++J) {
+                    bool any = !inw;
+                    for (int64_t j = J * TB; j < std::min<int64_t>(n, (J + 1) * TB) && !any; ++j) any = inw[j] != 0;
+                    if (any) tiles.push_back(J);
+                }
+                const int64_t nsw = (int64_t)tiles.size(), ring_wg = (int64_t)(ha[i].w + 1) * TT;
+                for (int64_t J : tiles) products += (T - J) * (int64_t)std::min<int64_t>(ha[i].w + 1, T - J);
+                int64_t cap = std::max<int64_t>(nsw, 1);
+                if (L.ring.n < cap * ring_wg) {
+                    size_t free_b = 0, total_b = 0;
+                    HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+                    const double room = 0.8 * (double)free_b + (double)L.ring.n * sizeof(double);
+                    cap = std::min<int64_t>(cap, (int64_t)(room / ((double)ring_wg * sizeof(double))));
+                    if (cap < 1) throw Refused("lsq_cov_band_windows: no device memory left for a window's sweeps");
+                    if (L.ring.n < cap * ring_wg) L.ring.alloc(cap * ring_wg);
+                }
+                cap = std::min<int64_t>(std::max<int64_t>(nsw, 1), L.ring.n / ring_wg);
+                grow(L.ssq, T * TB);
+                HIP_CHECK(hipMemsetAsync(L.ssq.p, 0, sizeof(double) * T * TB, st));
+                if (nsw > 0) {
+                    grow(L.tiles, nsw);
+                    L.tiles.upload(tiles.data(), nsw, st);
+                    run_sweeps<true>(st, ha[i], nsw, cap, L.tiles.p, nullptr, nullptr, nullptr, nullptr, W.sc.p, L.ring.p,
+                                     L.ssq.p);
+                }
+                hipLaunchKernelGGL(k_band_diag_sweep, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, nullptr, L.ssq.p, W.sc.p,
+                                   W.dE.p);
+                KERNEL_CHECK();
+                if (W.capE < n) {
+                    if (W.hE) HIP_CHECK(hipHostFree(W.hE));
+                    HIP_CHECK(hipHostMalloc(&W.hE, sizeof(double) * n));
+                    W.capE = n;
+                }
+                HIP_CHECK(hipMemcpyAsync(W.hE, W.dE.p, sizeof(double) * n, hipMemcpyDeviceToHost, st));
+                W.win = w;
+                W.n = n;
+                W.E = h_E + win_ptr[w];
+                W.inner = inw;
+                dev_bytes = std::max<int64_t>(dev_bytes, (int64_t)(W.R.n + W.RB.n) * (int64_t)sizeof(double));
+            }
+            HIP_CHECK(hipMemcpyAsync(L.herr, L.errs.p, sizeof(int) * 2 * nb, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipMemcpyAsync(L.herr + 2 * nbmax, L.errsB.p, sizeof(int) * 2 * nbmax, hipMemcpyDeviceToHost, st));
+            L.nin = nb;
+        }
+        for (BatchLane& L : lanes) batch_finish(L, nbmax);
+    } catch (...) {
+        for (BatchLane& L : lanes)
+            if (L.st) (void)hipStreamSynchronize(L.st);
+        throw;
+    }
+    if (info) {
+        info[0] = wmax_all;
+        info[1] = tmax;
+        info[2] = dev_bytes * nbmax * nl;
+        info[3] = products;
+        info[4] = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+        info[5] = nl;
+    }
+}
+
 void band_cov_windows(System& S, int64_t nwin, const int64_t* win_ptr, const int32_t* h_perm, const uint8_t* inner,
                       double* h_E, const int64_t* win_ops, const int64_t* op_ptr, const int32_t* op_pos,
                       const double* op_val, double* op_err, int64_t* info, const int64_t* bot_ptr,
@@ -1326,6 +1644,12 @@ void band_cov_windows(System& S, int64_t nwin, const int64_t* win_ptr, const int
                 for (int64_t e = op_ptr[i]; e < op_ptr[i + 1]; ++e)
                     if (op_pos[e] < 0 || op_pos[e] >= n)
                         throw std::invalid_argument("lsq_cov_band_windows: an op row reaches outside its window");
+    }
+    static const int fbatch = getenv("LSQ_E_FBATCH") ? std::max(1, std::min(atoi(getenv("LSQ_E_FBATCH")), 32)) : 8;
+    if (!win_ops && fbatch > 1 && nwin > 1) {   // identity sweeps only: windows in batches
+        band_cov_windows_batched(S, nwin, win_ptr, h_perm, inner, h_E, info, bot_ptr, bot_perm, nibs,
+                                 (int)std::min<int64_t>(fbatch, nwin));
+        return;
     }
     const int nl = [] {
         const char* e = getenv("LSQ_E_LANES");

@@ -193,3 +193,45 @@ def test_window_schur_split_equals_whole_window(gpu_available, name, tile, margi
     assert rel.max() <= 1e-9, rel.max()
     assert abs(c1 - c0) <= 1e-9 + 1e-6 * abs(c0)
     assert t1['E_window']['tile_products'] < t0['E_window']['tile_products']
+
+
+_CHILD_E = r'''
+import sys, json
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import lssurf_amd as LS
+from lssurf_amd import synthetic
+from lssurf_amd.constraint_functions import reference_epoch_keep_cols
+from lssurf_amd.errors import window_cov
+from lssurf_amd.smooth_fit import FitSystem
+D, kw = synthetic.points('t128')
+S = LS.smooth_fit(data=D, return_fit_objects=True, VERBOSE=False, **kw)
+keep = reference_epoch_keep_cols(S['G_data'].col_N, S['grids']['dz'], kw['reference_epoch'])
+fs = FitSystem(S['G_data'], S['Gc'], keep, S['Gc'].col_N, grids=S['grids'])
+w = 1. / np.concatenate((S['Ed'], S['Ec']))
+fs.solver.set_row_weight(w)
+fs.solver.set_row_mask(np.ones(w.size, bool))
+try:
+    E, _, c = window_cov(fs.solver, S['grids'], keep, tile=32, margin=24)
+finally:
+    fs.close()
+np.save(sys.argv[2], E)
+'''
+
+
+def test_window_batches_bit_identical(gpu_available, tmp_path):
+    """Windows factored in batches (one launch per step for LSQ_E_FBATCH windows, the default 8)
+    give σ bit for bit equal to one window at a time (LSQ_E_FBATCH=1): the same kernels on the
+    same bands.  Two child processes (the switch is read once per process)."""
+    import os
+    import subprocess
+    import sys
+    out = {}
+    for fb in ('1', '8'):
+        path = tmp_path / f'E{fb}.npy'
+        r = subprocess.run([sys.executable, '-c', _CHILD_E, os.path.dirname(__file__), str(path)],
+                           env=dict(os.environ, LSQ_E_FBATCH=fb), capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        out[fb] = np.load(path)
+    np.testing.assert_array_equal(out['1'], out['8'])
+    assert np.all(out['8'] > 0)
