@@ -50,7 +50,7 @@ def lump_by_node(D, node, slot):
     return sp.csr_matrix((Dc.data[ok], (Dc.row[ok], jn[ok])), shape=D.shape)
 
 
-def hierarchy(A, n_data_rows, keep_cols, ny, nx, nt, coarse=5):   # coarse: mg.inc MG_COARSE
+def hierarchy(A, n_data_rows, keep_cols, ny, nx, nt, coarse=5, coarse_cols=1024):   # mg.inc MG_COARSE, MG_COARSE_COLS
     """Levels [(shape, keep_mask_full, N_operator_full)] with N over each level's FULL column
     space (rows / columns of removed epochs zero).  Level 0: AᵀA; coarse: Galerkin stencil part +
     lumped data part."""
@@ -63,7 +63,7 @@ def hierarchy(A, n_data_rows, keep_cols, ny, nx, nt, coarse=5):   # coarse: mg.i
     Ns = (E @ (As.T @ As) @ E.T).tocsr()
     Nd = (E @ (Ad.T @ Ad) @ E.T).tocsr()
     levels = [((ny, nx), keep, (Ns + Nd).tocsr())]
-    while max(ny, nx) > coarse:
+    while max(ny, nx) > coarse and not (len(levels) > 1 and ny * nx * (1 + nt) <= coarse_cols):
         P, nyc, nxc = prolong_full(ny, nx, nt)
         Ns = (P.T @ Ns @ P).tocsr()
         Nd = lump_by_node((P.T @ Nd @ P).tocsr(), node_of(nyc, nxc, nt), slot_of(nyc, nxc, nt))
