@@ -385,12 +385,17 @@ __global__ __launch_bounds__(BLOCK) void k_block_factor_k(int64_t nb, double* __
 // R_b⁻¹ rounded to fp32 for CG's z = R_b⁻¹(R_b⁻ᵀ s): packed upper, block stride npks (npk rounded
 // up to even, so a run of blocks starts 8-byte aligned).  L L^T with a triangular L whose diagonal
 // is non-zero stays SPD whatever the rounding, so CG keeps a valid preconditioner at half the bytes.
-__global__ __launch_bounds__(BLOCK) void k_block_rinv32(int64_t nb, int npk, int npks, const double* __restrict__ Ri,
-                                                        lf_t* __restrict__ Lf) {
+// Lf = R_b⁻¹ rounded to lf_t; round_ri: Ri takes the rounded values too, so every consumer of the
+// system's block preconditioner (LSQR's epilogue from Lf, its x = M y and warm start from Ri, CGNR
+// from Lf) applies one and the same M
+__global__ __launch_bounds__(BLOCK) void k_block_rinv32(int64_t nb, int npk, int npks, double* __restrict__ Ri,
+                                                        lf_t* __restrict__ Lf, int round_ri) {
     for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < nb * npks; q += (int64_t)gridDim.x * BLOCK) {
         const int64_t b = q / npks;
         const int e = (int)(q - b * npks);
-        Lf[q] = e < npk ? lf_round(Ri[b * npk + e]) : lf_t(0);
+        const lf_t v = e < npk ? lf_round(Ri[b * npk + e]) : lf_t(0);
+        Lf[q] = v;
+        if (round_ri && e < npk) Ri[b * npk + e] = (double)lf_val(v);
     }
 }
 
@@ -608,7 +613,7 @@ void block_factor_in_place(System& S) {
         S.blk_Lf.alloc((int64_t)npks * S.nblk);
     }
     hipLaunchKernelGGL(k_block_rinv32, dim3(grid_for(S.nblk * npks)), dim3(BLOCK), 0, S.stream, S.nblk, npk, npks,
-                       S.blk_Ri.p, S.blk_Lf.p);
+                       S.blk_Ri.p, S.blk_Lf.p, 1);
     KERNEL_CHECK();
     HIP_CHECK(hipStreamSynchronize(S.stream));
     S.blk_valid = true;
@@ -630,7 +635,7 @@ void block_factor_packed(int64_t nb, const int64_t* ptr, int kmax, double* Ri, l
         hipLaunchKernelGGL(k_block_factor, dim3(grid_for(nb)), dim3(BLOCK), 0, st, nb, ptr, kmax, Ri, ndead);
     KERNEL_CHECK();
     const int npk = kmax * (kmax + 1) / 2, npks = lf_stride(npk);
-    hipLaunchKernelGGL(k_block_rinv32, dim3(grid_for(nb * npks)), dim3(BLOCK), 0, st, nb, npk, npks, Ri, Lf);
+    hipLaunchKernelGGL(k_block_rinv32, dim3(grid_for(nb * npks)), dim3(BLOCK), 0, st, nb, npk, npks, Ri, Lf, 0);
     KERNEL_CHECK();
 }
 

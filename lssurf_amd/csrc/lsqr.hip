@@ -409,6 +409,14 @@ Grids grids_for(const System& S) {
         g.gS = (int)std::min<int64_t>(std::max<int64_t>(S.mfh.nodes / MF_ALIGN, 1), NPART - g.gD);
         g.gM = (int)std::min<int64_t>(std::max<int64_t>(S.mfh.nodes / (SELL_C * MF_NPT) / 4, 1), NPART);
         g.gXf = grid_for(S.n_full, BLOCK * 4, NPART);
+        if (MF_AT_SPLIT)     // Aᵀu: one column group per workgroup step
+            g.gM = (int)std::min<int64_t>(std::max<int64_t>(S.mfh.nodes / (SELL_C * MF_NPT), 1), NPART);
+        if (MF_FWD_ROWS) {   // A·v by rows: no staged bands; segments on multiples of 8 (XCD order)
+            g.lds = 0;
+            g.gXf = (g.gXf + 7) / 8 * 8;
+            g.gD = (g.gD + 7) / 8 * 8;
+            g.gS = std::max(1, std::min<int>((int)std::min<int64_t>(S.mfh.rchunks, NPART - g.gD) / 8 * 8, NPART - g.gD));
+        }
     }
     g.gA = (int)std::min<int64_t>(std::max<int64_t>((S.A.nslices + 3) / 4, 1), NPART);
     g.gT = (int)std::min<int64_t>(std::max<int64_t>((S.AT.nslices + 3) / 4, 1), NPART);
@@ -766,16 +774,18 @@ void mf_column_scale(System& S, bool raw) {
 // Bytes per LSQR iteration with preconditioner `precond`.  Block-Jacobi (3): Aᵀu writes the raw
 // t = Aᵀũ (8 B per column instead of cs, ṽ in, ṽ out and zv: 24 B less per column of the
 // structured v-space, 8 B less on the assembled one) and the epilogue k_block_epi(_aff) reads t,
-// ṽ, writes ṽ', z (32 B per block column) and streams the f64 factor (8·npk per block).
+// ṽ, writes ṽ', z (32 B per block column) and streams the factor: the lf_t copy (sizeof(lf_t)·npks
+// per block, k_block_epi_lf) or the f64 one (8·npk).
 double bytes_per_iter(const System& S, bool mf, int precond) {
     double b[2];
     kernel_bytes(S, mf, b);
     double tot = b[0] + b[1];
     if (precond == 3 && S.nblk > 0) {
-        const double npk = (double)S.blk_kmax * (S.blk_kmax + 1) / 2;
+        const int npk = S.blk_kmax * (S.blk_kmax + 1) / 2;
         const double ncol = S.blk_affine ? (double)S.nblk * S.blk_kmax : (double)S.G.n;
+        const double fac = block_epi_lf(S, mf) ? (double)sizeof(lf_t) * lf_stride(npk) : 8.0 * npk;
         tot -= mf ? 24.0 * (double)S.n_full : 8.0 * (double)S.G.n;
-        tot += 32.0 * ncol + 8.0 * npk * (double)S.nblk;
+        tot += 32.0 * ncol + fac * (double)S.nblk;
     }
     return tot;
 }

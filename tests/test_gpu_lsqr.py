@@ -376,3 +376,46 @@ def test_column_blocks_validation(gpu_available):
     finally:
         fs.close()
     assert np.linalg.norm(x - x1) / np.linalg.norm(x1) <= 1e-8
+
+
+_CHILD_EPI = r'''
+import sys, json
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from test_gpu_lsqr import _t64_blocks
+S, fs, w, rhs = _t64_blocks()
+keep = np.ones(fs.n_data, bool)
+tol = dict(atol=1e-12, btol=1e-12, conlim=1e12)
+try:
+    x = fs.solve(w, keep, rhs, precond=3, **tol)
+    st = dict(fs.stats)
+    xw = fs.solve(w, keep, rhs, x0=x * (1 + 1e-3), precond=3, **tol)
+    stw = dict(fs.stats)
+finally:
+    fs.close()
+np.savez(sys.argv[2], x=x, xw=xw)
+print(json.dumps({'iters': int(st['iters']), 'iters_w': int(stw['iters']), 'bytes': float(st['bytes_per_iter'])}))
+'''
+
+
+def test_block_epilogue_lf_factor_bit_identical(gpu_available, tmp_path):
+    """LSQR + block-Jacobi on the structured operator: the epilogue streaming the lf_t (bf16) factor
+    copy gives x bit for bit equal to the f64-factor epilogue (LSQ_BLOCK_EPI_LF=0) — blk_Ri holds the
+    rounded values, so both apply the same M — with the same iteration counts, cold and warm, and
+    fewer algorithmic bytes per iteration.  Child processes (the switch is read once per process)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    out = {}
+    for lf in ('1', '0'):
+        path = tmp_path / f'x{lf}.npz'
+        r = subprocess.run([sys.executable, '-c', _CHILD_EPI, os.path.dirname(__file__), str(path)],
+                           env=dict(os.environ, LSQ_BLOCK_EPI_LF=lf), capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        out[lf] = (dict(np.load(path)), json.loads(r.stdout.strip().splitlines()[-1]))
+    (a, sa), (b, sb) = out['1'], out['0']
+    np.testing.assert_array_equal(a['x'], b['x'])
+    np.testing.assert_array_equal(a['xw'], b['xw'])
+    assert sa['iters'] == sb['iters'] and sa['iters_w'] == sb['iters_w'], (sa, sb)
+    assert sa['bytes'] < sb['bytes'], (sa, sb)

@@ -28,6 +28,7 @@ EOF
 done
 cp tools/ab/lib_base.so lssurf_amd/liblsqsurf.so
 # SQ / TCC counters of the base build's LSQR kernels (separate passes, kernel-trace only)
+[ -n "${SKIP_PMC:-}" ] && exit 0
 timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES -d $OUT/pmc_sq -o run --output-format csv -- python3 bench.py --method lsqr --no-cpu --no-pmc --no-solve --steps 20 --warmup 2 > $OUT/pmc_sq.log 2>&1 || { echo "pmc sq failed"; tail -5 $OUT/pmc_sq.log; exit 1; }
 python3 tools/pmc_summary.py $OUT/pmc_sq k_mf_ k_block_epi > $OUT/pmc_sq.txt && cat $OUT/pmc_sq.txt
 timeout -k 10 -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --method lsqr --no-cpu --no-pmc --no-solve --steps 20 --warmup 2 > $OUT/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; tail -5 $OUT/pmc_fetch.log; exit 1; }
