@@ -245,7 +245,6 @@ bool describe_stencil_operator(MfDesc& d, int64_t m, int64_t n_full, int32_t n_g
         }
         P.var = S.F ? 1 : 0;
         P.F = S.F;
-        for (int k = 0; k < 3; ++k) P.bfd[k] = make_fastdiv((uint32_t)(P.hi[k] - P.lo[k]));
         P.nfield = 0;
         for (int t = 0; t < S.ntpl; ++t) P.nfield = std::max(P.nfield, P.fsel[t] + 1);
         // Aᵀu validity of template t for a column c: lo <= c - off_t < hi in every dim, i.e.
@@ -316,15 +315,6 @@ bool describe_stencil_operator(MfDesc& d, int64_t m, int64_t n_full, int32_t n_g
         }
     }
     d.nodes = node0;
-    d.rchunks = 0;
-    for (int g = 0; g < n_grids; ++g) {   // A·v by rows: chunk i of every part of a grid, then i + 1
-        MfGrid& G = d.g[g];
-        G.rch = 0;
-        for (int q = 0; q < G.nparts; ++q)
-            G.rch = std::max<int32_t>(G.rch, (d.p[G.part[q]].n_eq + MF_RCH - 1) / MF_RCH);
-        G.rch0 = (int32_t)d.rchunks;
-        d.rchunks += (int64_t)G.rch * G.nparts;
-    }
     return d.n_parts > 0 && covered == n_full && node0 < (int64_t(1) << 31);
 }
 

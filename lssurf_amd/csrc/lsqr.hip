@@ -409,14 +409,6 @@ Grids grids_for(const System& S) {
         g.gS = (int)std::min<int64_t>(std::max<int64_t>(S.mfh.nodes / MF_ALIGN, 1), NPART - g.gD);
         g.gM = (int)std::min<int64_t>(std::max<int64_t>(S.mfh.nodes / (SELL_C * MF_NPT) / 4, 1), NPART);
         g.gXf = grid_for(S.n_full, BLOCK * 4, NPART);
-        if (MF_AT_SPLIT)     // Aᵀu: one column group per workgroup step
-            g.gM = (int)std::min<int64_t>(std::max<int64_t>(S.mfh.nodes / (SELL_C * MF_NPT), 1), NPART);
-        if (MF_FWD_ROWS) {   // A·v by rows: no staged bands; segments on multiples of 8 (XCD order)
-            g.lds = 0;
-            g.gXf = (g.gXf + 7) / 8 * 8;
-            g.gD = (g.gD + 7) / 8 * 8;
-            g.gS = std::max(1, std::min<int>((int)std::min<int64_t>(S.mfh.rchunks, NPART - g.gD) / 8 * 8, NPART - g.gD));
-        }
     }
     g.gA = (int)std::min<int64_t>(std::max<int64_t>((S.A.nslices + 3) / 4, 1), NPART);
     g.gT = (int)std::min<int64_t>(std::max<int64_t>((S.AT.nslices + 3) / 4, 1), NPART);

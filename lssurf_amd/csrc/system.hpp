@@ -63,8 +63,6 @@ constexpr int MF_NPT = 2;                    // nodes per thread per block itera
 constexpr int MF_ALIGN = 256 * MF_NPT;       // node-enumeration alignment of every grid
 constexpr int MF_R = 3;                      // |template offset| <= MF_R (8 edge classes per side)
 constexpr int MF_LDS_MAX = 4096;             // doubles of LDS per block for the A·v staging (32 KB)
-constexpr int MF_RPT = 2;                    // A·v by rows: rows per thread of a chunk
-constexpr int MF_RCH = 256 * MF_RPT;         // A·v by rows: rows per chunk (one part's)
 struct FastDiv {            // n / d for 0 <= n < 2^31: (n * mul) >> (32 + shift)
     uint64_t mul;
     uint32_t shift, d;
@@ -99,7 +97,6 @@ struct MfPart {
     int32_t fsel[MF_MAXT];                   // field-valued parts: field of template t
     int32_t nfield, pad2;
     const double* F;                         // field-valued parts: nfield × n_eq (device)
-    FastDiv bfd[3];                          // box extents hi − lo (A·v by rows: row → centre)
 };
 struct MfGrid {
     int32_t ndim, nparts;
@@ -110,13 +107,10 @@ struct MfGrid {
     // distinct template y offset, covering the in-row offsets [emin, emax] of that offset
     int32_t nband, lds;                      // lds = doubles staged (0: gather from HBM)
     int32_t band_oy[2 * MF_R + 1], band_emin[2 * MF_R + 1], band_len[2 * MF_R + 1], band_start[2 * MF_R + 1];
-    int32_t rch, rch0;                       // A·v by rows: MF_RCH-row chunks of the longest part; first
-                                             // chunk of this grid (its chunks interleave its parts)
 };
 struct MfDesc {
     int32_t n_grids, n_parts;
     int64_t nodes;                 // end of the node enumeration (grids with parts, MF_ALIGN-aligned)
-    int64_t rchunks;               // A·v by rows: Σ over grids of rch · nparts
     int64_t npts, m, n_full;
     MfGrid g[MF_MAX_GRIDS];
     MfPart p[MF_MAX_PARTS];
