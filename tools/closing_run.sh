@@ -1,7 +1,7 @@
-# round 6 final: the whole GPU suite and smoke() on the final tree, the default bench, the rocprofv3
+# Closing run (the round-6 one): the whole GPU suite and smoke() on the final tree, the default bench, the rocprofv3
 # kernel-trace statistics of the bench command, and the torchrun path at N = 2 on the one card
 set -uo pipefail
-OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r6f}
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-closing}
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp

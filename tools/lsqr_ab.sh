@@ -1,7 +1,7 @@
-# round 6: LSQR operator kernels — occupancy variants (tools/ab/lib_<v>.so) against the base build,
+# LSQR A/B on one GPU box: variants tools/ab/lib_<v>.so (tools/build_variant.sh) against tools/ab/lib_base.so,
 # alternating on one box: LSQR + block-Jacobi it/s at C4, then a rocprofv3 kernel-trace of each
 set -uo pipefail
-OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r6i}
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-lsqr_ab}
 shift || true
 V="${*:-at6 fwd8}"
 mkdir -p $OUT
