@@ -164,7 +164,9 @@ int lsq_set_row_mask(lsq_handle* h, const uint8_t* keep);
  * columns cols[block_ptr[b] .. block_ptr[b+1]) (at most 16, each column in at most one block);
  * unlisted columns are singleton blocks.  For smooth_fit a block is one (y, x) node: its z0
  * column and its dz columns of every kept epoch.  The factors R_b (AᵀA restricted to the block
- * = R_bᵀR_b, with the current row weights / mask) are rebuilt on the device when weights change.
+ * = R_bᵀR_b, with the current row weights / mask) are rebuilt on the device when weights change;
+ * R_b⁻¹ is kept rounded to bf16 (products in f64), the same M for CGNR and for every use LSQR
+ * makes of it, so x is unaffected (any non-singular M gives the same least-squares solution).
  * NULL / 0 blocks clears the structure (every column its own block).  On a structured rank
  * (lsq_dist_set_halo) the blocks are the rank's owned nodes in its local compact ids, factored
  * from the rank's own rows; ghost columns stay outside every block. */
