@@ -399,7 +399,9 @@ struct Grids {
 Grids grids_for(const System& S) {
     Grids g;
     g.gD = g.gS = g.gM = g.gXf = 1;
-    g.gB = grid_for(std::max<int64_t>(S.nblk, 1) * 16, BLOCK, NPART);   // 16 lanes per column block
+    // block-Jacobi epilogue: at most 1 024 workgroups (two thirds of one dispatch round at its 6 waves
+    // per SIMD; 2 048 took 1.3 rounds): LSQR at C4 846–848 → 860–862 it/s (profiles/r06_lsqr_epi_ab.txt)
+    g.gB = grid_for(std::max<int64_t>(S.nblk, 1) * 16, BLOCK, 1024);   // 16 lanes per column block
     g.lds = 0;
     if (S.mf)
         for (int k = 0; k < S.mfh.n_grids; ++k) g.lds = std::max<size_t>(g.lds, sizeof(double) * S.mfh.g[k].lds);
