@@ -7,7 +7,9 @@ XZERO step on it, so the level-0 V-cycle applied to the same vector, the CGNR + 
 iteration count and the solution agree to rounding (≤ 1e-12 relative; the run also reports
 whether they are bitwise equal), and the solve reaches the golden exact solution (DESIGN.md
 tolerances).  Systems: t64, t256 (the BASELINE layout), sf3d_eq_edit and deep1 (the 48²×12 depth
-golden, a ≥ 4-level hierarchy)."""
+golden, a ≥ 4-level hierarchy).  LSQ_MG_FUSE=13 adds bit 3: on the direct-kernel levels the
+operator kernel writes the residual r − N_s x − B x itself (the smoother's MG_RES order) instead of
+q, and the separate residual pass is dropped."""
 import json
 import os
 import subprocess
@@ -73,8 +75,9 @@ def _run(tmp_path, tag, env_extra):
     return json.load(open(out))
 
 
-def test_restrict_smooth_fusion_equals_separate_launches(gpu_available, tmp_path):
-    on = _run(tmp_path, 'on', {'LSQ_MG_FUSE': '5'})
+@pytest.mark.parametrize('fuse', ['5', '13'])
+def test_restrict_smooth_fusion_equals_separate_launches(gpu_available, tmp_path, fuse):
+    on = _run(tmp_path, 'on', {'LSQ_MG_FUSE': fuse})
     off = _run(tmp_path, 'off', {'LSQ_MG_FUSE': '1'})
     report = {}
     for name in on:
@@ -88,4 +91,4 @@ def test_restrict_smooth_fusion_equals_separate_launches(gpu_available, tmp_path
         assert np.linalg.norm(xa - xb) <= 1e-12 * np.linalg.norm(xb), name
         if 'rel' in a:
             assert a['rel'] <= 1e-6, (name, a['rel'])
-    print('rsfuse', json.dumps(report))
+    print('rsfuse', fuse, json.dumps(report))
